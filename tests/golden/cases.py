@@ -1,0 +1,74 @@
+"""Golden-case definitions shared by the fixture generator (make_golden.py) and the parity tests.
+
+Pure data/helpers: no reference import, so the GPU-box tests can rebuild the exact same inputs.
+Synthetic token ids follow the wrapper templates of qwen_tts/inference/qwen3_tts_model.py:269-276
+(`<|im_start|>assistant\n{text}<|im_end|>\n<|im_start|>assistant\n` etc.; no BPE offline).
+"""
+import numpy as np
+import torch
+
+
+def text_ids(n, seed):
+    g = np.random.default_rng([seed, 7])
+    body = g.integers(1000, 150000, n).tolist()
+    return torch.tensor([[151644, 77091, 198] + body + [151645, 198, 151644, 77091, 198]], dtype=torch.long)
+
+
+def instruct_ids(n, seed):
+    g = np.random.default_rng([seed, 11])
+    return torch.tensor([[151644, 872, 198] + g.integers(1000, 150000, n).tolist() + [151645, 198]],
+                        dtype=torch.long)
+
+
+def ref_text_ids(n, seed):
+    g = np.random.default_rng([seed, 13])
+    return torch.tensor([[151644, 77091, 198] + g.integers(1000, 150000, n).tolist() + [151645, 198]],
+                        dtype=torch.long)
+
+
+def talker_cases():
+    """Prompt layouts covering SURVEY.md §8a G1/G2 and Appendix A (each case = kwargs of generate)."""
+    return {
+        "cv_b1_nonstream": dict(texts=[9], languages=["english"], speakers=["vivian"], non_streaming_mode=True,
+                                max_new_tokens=13),
+        "cv_b2_stream_dialect": dict(texts=[12, 5], languages=["chinese", "auto"], speakers=["eric", "ryan"],
+                                     non_streaming_mode=False, max_new_tokens=16),
+        "cv_b3_auto_nospk": dict(texts=[7, 3, 10], languages=["auto", "english", "japanese"],
+                                 speakers=["", None, "dylan"], non_streaming_mode=False, max_new_tokens=12),
+        "vd_b2_instruct": dict(texts=[6, 11], languages=["english", "auto"], speakers=None, instruct=[8, 0],
+                               non_streaming_mode=True, max_new_tokens=10),
+        "cv_b2_sample": dict(texts=[8, 4], languages=["english", "chinese"], speakers=["vivian", "ryan"],
+                             non_streaming_mode=False, max_new_tokens=10, do_sample=True,
+                             subtalker_dosample=True, seed=77),
+        "icl_b2": dict(texts=[6, 9], languages=["english", "auto"], speakers=None, non_streaming_mode=False,
+                       max_new_tokens=10, icl=[(5, 7, True, False), (12, 4, False, True)]),
+        "icl_b1_nonstream": dict(texts=[5], languages=["english"], speakers=None, non_streaming_mode=True,
+                                 max_new_tokens=8, icl=[(4, 6, True, False)]),
+    }
+
+
+def make_inputs(case, idx, H):
+    ids = [text_ids(n, 100 * idx + j) for j, n in enumerate(case["texts"])]
+    ins = None
+    if "instruct" in case:
+        ins = [instruct_ids(n, 200 * idx + j) if n else None for j, n in enumerate(case["instruct"])]
+    vcp, ref_ids = None, None
+    if "icl" in case:
+        g = np.random.default_rng([idx, 17])
+        vcp = dict(ref_code=[], ref_spk_embedding=[], x_vector_only_mode=[], icl_mode=[])
+        ref_ids = []
+        for j, (nref, ncode, icl, xvec) in enumerate(case["icl"]):
+            vcp["ref_code"].append(torch.tensor(g.integers(0, 2048, (ncode, 16)), dtype=torch.long) if icl else None)
+            vcp["ref_spk_embedding"].append(torch.tensor(0.02 * g.standard_normal(H), dtype=torch.float32))
+            vcp["x_vector_only_mode"].append(xvec)
+            vcp["icl_mode"].append(icl)
+            ref_ids.append(ref_text_ids(nref, 300 * idx + j))
+    return ids, ins, vcp, ref_ids
+
+
+def gen_kwargs(case):
+    return dict(max_new_tokens=case["max_new_tokens"], do_sample=case.get("do_sample", False),
+                subtalker_dosample=case.get("subtalker_dosample", False), top_k=50, top_p=1.0, temperature=0.9,
+                subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9, repetition_penalty=1.05)
+
+

@@ -1,0 +1,223 @@
+"""Generate golden vectors by running the REFERENCE (`/root/reference/qwen_tts`) in this container.
+
+    python tests/golden/make_golden.py            # tiny talker + tiny/full codec fixtures
+    python tests/golden/make_golden.py --full     # + full ASSUMED-dim 1.7B greedy codes (slow, ~16 GB RAM)
+
+Test infrastructure only: needs /root/reference (absent on the GPU box).  The reference is imported
+through tests/golden/ref_shim.py (transformers-5.15 -> 4.57 patches).  Weights are the
+seeded synthetic ones of oracle/weights.py loaded into the reference modules by state_dict name, so the
+oracle and the HIP path can regenerate identical weights without the fixture storing them.
+
+Fixtures written (inputs + expected outputs only):
+  tiny_talker.npz   greedy / sampled / EOS / ICL generate() codes for several prompt layouts
+  codec_*.npz       12 Hz decoder PCM for fixed codes (single, right-padded batch, chunked > 300 frames)
+  param_specs.json  reference state_dict names and shapes per preset (the checkpoint key contract)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+
+import ref_shim  # noqa: E402
+from cases import gen_kwargs, make_inputs, talker_cases  # noqa: E402,F401
+from oracle import load_preset  # noqa: E402
+from oracle.weights import synth_param  # noqa: E402
+
+SEED = 1234
+
+
+def _eagerize(c):
+    c._attn_implementation = "eager"
+    c.pad_token_id = None
+
+
+def build_ref_model(name, seed=SEED, meta=False):
+    mdl, cfgm, _, _ = ref_shim.load_reference()
+    cfg, _ = load_preset(name)
+    config = cfgm.Qwen3TTSConfig(**json.loads(json.dumps(cfg)))
+    for c in (config, config.talker_config, config.talker_config.code_predictor_config):
+        _eagerize(c)
+    if meta:
+        with torch.device("meta"):
+            return mdl.Qwen3TTSForConditionalGeneration(config), cfg
+    torch.manual_seed(0)
+    model = mdl.Qwen3TTSForConditionalGeneration(config).eval()
+    sd = model.state_dict()
+    new = {k: torch.from_numpy(synth_param(k, v.shape, seed)) for k, v in sd.items()}
+    model.load_state_dict(new)
+    return model, cfg
+
+
+def build_ref_codec(name, seed=SEED, meta=False):
+    _, _, mtok, ctok = ref_shim.load_reference()
+    _, ccfg = load_preset(name)
+    config = ctok.Qwen3TTSTokenizerV2Config(**json.loads(json.dumps(ccfg)))
+    dc = config.decoder_config
+    _eagerize(dc)
+    ctx = torch.device("meta") if meta else torch.device("cpu")
+    with ctx:
+        dec = mtok.Qwen3TTSTokenizerV2Decoder(dc).eval()
+    if meta:
+        return dec, ccfg
+    sd = dec.state_dict()
+    dec.load_state_dict({k: torch.from_numpy(synth_param("decoder." + k, v.shape, seed)) for k, v in sd.items()})
+    return dec, ccfg
+
+
+class _CodecModelView:
+    """The attributes Qwen3TTSTokenizerV2Model.decode reads (K:992-1022), so the reference method itself runs."""
+
+    def __init__(self, decoder, ccfg):
+        class C:
+            return_dict = True
+        self.config = C()
+        self.decoder = decoder
+        self.decode_upsample_rate = ccfg["decode_upsample_rate"]
+
+
+def ref_codec_decode(dec, ccfg, codes_list):
+    """Qwen3TTSTokenizer.decode list path (Z:259-365) on top of the reference V2Model.decode."""
+    _, _, mtok, _ = ref_shim.load_reference()
+    codes = [torch.as_tensor(c, dtype=torch.long) for c in codes_list]
+    padded = torch.nn.utils.rnn.pad_sequence(codes, batch_first=True, padding_value=0)
+    with torch.inference_mode():
+        out = mtok.Qwen3TTSTokenizerV2Model.decode(_CodecModelView(dec, ccfg), padded, return_dict=True)
+    return [w.to(torch.float32).numpy() for w in out.audio_values]
+
+
+def run_ref_generate(model, case, idx, H):
+    ids, ins, vcp, ref_ids = make_inputs(case, idx, H)
+    torch.manual_seed(case.get("seed", 0))
+    with torch.no_grad():
+        codes, hid = model.generate(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp,
+                                    languages=case["languages"], speakers=case["speakers"],
+                                    non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+    return codes, hid
+
+
+def pack_case(out, key, case, codes, hid):
+    out[f"{key}/n"] = np.array(len(codes))
+    for j, (c, h) in enumerate(zip(codes, hid)):
+        out[f"{key}/codes{j}"] = c.numpy().astype(np.int32)
+        out[f"{key}/hidden{j}"] = h.numpy().astype(np.float32)
+
+
+def make_tiny_talker(preset="tiny-customvoice"):
+    model, cfg = build_ref_model(preset)
+    H = cfg["talker_config"]["hidden_size"]
+    out = {}
+    cases = talker_cases()
+    for idx, (key, case) in enumerate(cases.items()):
+        if key.startswith("vd_"):
+            continue  # voice-design preset below (only the wrapper differs; generate() is the same)
+        t0 = time.time()
+        codes, hid = run_ref_generate(model, case, idx, H)
+        pack_case(out, key, case, codes, hid)
+        print(f"  {key}: frames {[c.shape[0] for c in codes]} ({time.time() - t0:.1f}s)")
+    vd_model, _ = build_ref_model("tiny-voicedesign")
+    for idx, (key, case) in enumerate(cases.items()):
+        if key.startswith("vd_"):
+            codes, hid = run_ref_generate(vd_model, case, idx, H)
+            pack_case(out, key, case, codes, hid)
+            print(f"  {key}: frames {[c.shape[0] for c in codes]}")
+    # EOS case: copy a frequently chosen cb0 row into the EOS row of codec_head so EOS wins the second time
+    # that token would be picked (repetition penalty divides the repeated one) -> early, ragged stops.
+    eos = cfg["talker_config"]["codec_eos_token_id"]
+    key, case = "cv_b2_stream_dialect", cases["cv_b2_stream_dialect"]
+    c0 = torch.cat([torch.from_numpy(out[f"{key}/codes{j}"][:, 0]) for j in range(2)])
+    vals, counts = torch.unique(c0, return_counts=True)
+    donor = int(vals[torch.argmax(counts)])
+    with torch.no_grad():
+        model.talker.codec_head.weight[eos] = model.talker.codec_head.weight[donor]
+    case = dict(case, max_new_tokens=24)
+    codes, hid = run_ref_generate(model, case, list(cases).index(key), H)
+    pack_case(out, "eos_b2", case, codes, hid)
+    out["eos_b2/donor"] = np.array(donor)
+    print(f"  eos_b2 (donor {donor}): frames {[c.shape[0] for c in codes]}")
+    np.savez_compressed(os.path.join(HERE, "tiny_talker.npz"), **out)
+
+
+def make_codec(preset, cases, fname):
+    dec, ccfg = build_ref_codec(preset)
+    out = {}
+    g = np.random.default_rng(4321)
+    for key, lens in cases.items():
+        codes = [g.integers(0, 2048, (n, 16)).astype(np.int64) for n in lens]
+        codes[0][min(3, lens[0] - 1), 0] = 0  # a legit cb0 == 0 shortens the output (quirk C0-3)
+        t0 = time.time()
+        wavs = ref_codec_decode(dec, ccfg, codes)
+        for j, (c, w) in enumerate(zip(codes, wavs)):
+            out[f"{key}/codes{j}"] = c.astype(np.int32)
+            out[f"{key}/len{j}"] = np.array(w.shape[0])
+            if w.shape[0] > 200_000:  # keep fixtures small: strided samples + checksums for long outputs
+                out[f"{key}/wav{j}_stride"] = w[::7].copy()
+                out[f"{key}/wav{j}_sum"] = np.array([w.astype(np.float64).sum(), (w.astype(np.float64) ** 2).sum()])
+            else:
+                out[f"{key}/wav{j}"] = w
+        print(f"  {fname}:{key} lens {[w.shape[0] for w in wavs]} ({time.time() - t0:.1f}s)")
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+
+
+def make_specs():
+    specs = {}
+    for p in ("tiny-customvoice", "tiny-base", "1.7b-customvoice", "0.6b-customvoice"):
+        m, _ = build_ref_model(p, meta=True)
+        specs[p] = {k: list(v.shape) for k, v in m.state_dict().items()}
+        d, _ = build_ref_codec(p, meta=True)
+        specs[p + "/codec"] = {"decoder." + k: list(v.shape) for k, v in d.state_dict().items()}
+    with open(os.path.join(HERE, "param_specs.json"), "w") as f:
+        json.dump(specs, f)
+
+
+def make_full(preset="1.7b-customvoice", frames=32):
+    t0 = time.time()
+    model, cfg = build_ref_model(preset)
+    print(f"  built {preset} in {time.time() - t0:.0f}s")
+    H = cfg["talker_config"]["hidden_size"]
+    out = {}
+    for key, case in {"full_b1": dict(texts=[120], languages=["english"], speakers=["vivian"],
+                                      non_streaming_mode=True, max_new_tokens=frames + 1),
+                      "full_b4_stream": dict(texts=[40, 25, 33, 18], languages=["english"] * 4,
+                                             speakers=["vivian", "ryan", "serena", "aiden"],
+                                             non_streaming_mode=False, max_new_tokens=frames + 1)}.items():
+        t0 = time.time()
+        codes, hid = run_ref_generate(model, case, 50 + len(out), H)
+        out[f"{key}/n"] = np.array(len(codes))
+        for j, c in enumerate(codes):
+            out[f"{key}/codes{j}"] = c.numpy().astype(np.int32)
+            out[f"{key}/hidden{j}_first"] = hid[j][:2].numpy().astype(np.float32)
+        print(f"  {key}: frames {[c.shape[0] for c in codes]} ({time.time() - t0:.0f}s)")
+    np.savez_compressed(os.path.join(HERE, f"full_{preset}.npz"), **out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--full", action="store_true")
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    torch.set_num_threads(8)
+    if a.only in (None, "specs"):
+        make_specs()
+    if a.only in (None, "talker"):
+        make_tiny_talker()
+    if a.only in (None, "codec"):
+        make_codec("tiny-customvoice", {"single": [40], "batch_ragged": [23, 9], "chunked": [330]},
+                   "codec_tiny.npz")
+        make_codec("1.7b-customvoice", {"single": [38], "batch_ragged": [12, 5]}, "codec_full.npz")
+    if a.full or a.only == "full":
+        make_full()
+
+
+if __name__ == "__main__":
+    main()
