@@ -1,0 +1,155 @@
+/*
+ * qwen3tts_amd.h -- C ABI of the MI355X-native (gfx950) Qwen3-TTS hot path.
+ *
+ * Library: qwen3-tts_amd/lib/libqwen3tts_amd.so (built by qwen3-tts_amd/build.py / __graft_entry__.build()).
+ *
+ * The reference (kritsanan1/Qwen3-TTS = QwenLM/Qwen3-TTS 0.0.4) has NO native ABI: its hot path is PyTorch
+ * eager code plus third-party kernels reached through nn.Linear / transformers' ALL_ATTENTION_FUNCTIONS
+ * (SURVEY.md §2, §8b).  Each entry point below names the reference operator(s) it replaces
+ * (M = qwen_tts/core/models/modeling_qwen3_tts.py, K = qwen_tts/core/tokenizer_12hz/modeling_qwen3_tts_tokenizer_v2.py).
+ *
+ * Conventions: plain device pointers + sizes, a hipStream_t passed as void*, int status return
+ * (0 = ok, < 0 = QT_ERR_*; qt_last_error() is not needed: codes are exhaustive).  No allocation, no host
+ * synchronisation, no global mutable state: every call is graph-capturable and reentrant.
+ * Activations: row-major, channels-last.  dtype codes: QT_F32 / QT_BF16.
+ */
+#ifndef QWEN3TTS_AMD_H
+#define QWEN3TTS_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { QT_F32 = 0, QT_BF16 = 1 };
+enum { QT_ACT_NONE = 0, QT_ACT_SILU = 1, QT_ACT_GELU = 2 };
+enum { QT_EPI_STORE = 0, QT_EPI_ADD = 1, QT_EPI_SWIGLU = 2 };
+enum { QT_OK = 0, QT_ERR_ARG = -1, QT_ERR_SHAPE = -2, QT_ERR_DTYPE = -3, QT_ERR_LAUNCH = -4 };
+
+/* ---------------------------------------------------------------------------------------------
+ * qt_gemm: out[m][n] (=|+=) epi( rs[m] * sum_k W[n][k] * gamma[k] * A[m][k] + bias[n] ) * colscale[n]
+ *
+ * Replaces every nn.Linear / nn.Conv1d / nn.ConvTranspose1d of the hot path:
+ *   talker & code predictor q/k/v/o, gate/up/down, codec_head, lm_head[g], small_to_mtp_projection,
+ *   text_projection (M:740-751, 848-850, 1167-1174, 1575-1579);  codec pre_conv, transformer linears,
+ *   ConvNeXt pwconv, decoder convs / transposed convs (K:159-242, 294-369, 492-493, 618-657, 838-864).
+ * Fused prologues: RMSNorm (gamma != NULL; Qwen3TTSRMSNorm M:595-610 feeding the Linear), row gather
+ * (a_index != NULL; nn.Embedding feeding the Linear), implicit im2col (taps > 0).
+ * Fused epilogues: bias, SiLU / GELU, colscale (LayerScale K:393-405, ConvNeXt gamma K:236),
+ * residual add (QT_EPI_ADD, M:1409/1417), SwiGLU (QT_EPI_SWIGLU; W rows interleaved 8 gate / 8 up per
+ * 16-row tile, output width N/2; Qwen3TTSTalkerTextMLP M:842-855).
+ * W must be pre-tiled by qt_tile_weight (layout in gemm.hip; rows padded to 16).  Columns n >= N are not
+ * written (SwiGLU: N = 2*I, I % 8 == 0).
+ * Conv mode (taps > 0): A is [batch][t_in][cin] (lda = row stride), output row m = b*t_out + t reads
+ * input time t + t_off + j*dil for tap j (zero outside [0, t_in)), K = taps*cin_pad.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_gemm_args {
+  int M, N, K;
+  int a_dtype, w_dtype, o_dtype;
+  const void* A;
+  long long lda;
+  const int* a_index;
+  const void* W;
+  const float* gamma;
+  float eps;
+  const float* bias;
+  const float* colscale;
+  int act;
+  int epi;
+  void* out;
+  long long ldo;
+  int taps, dil, cin, cin_pad, t_in, t_out, t_off;
+} qt_gemm_args;
+
+int qt_gemm(const qt_gemm_args* args, void* stream);
+
+/* Row-major [N][Kp] weight (Kp padded to 32 bf16 / 16 fp32) -> MFMA-fragment tiles (ceil(N/16)*16 rows). */
+int qt_tile_weight(const void* src, int dtype, int N, int Kp, void* dst, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * qt_qkv_post: per-head q_norm / k_norm (RMSNorm over head_dim), rotate-half RoPE from cos/sin tables,
+ * q written to q_out (fp32 [R][Hq*D]); k, v written into the KV cache at (row_batch[r], kv_pos[r]).
+ * Replaces M:773-785 (q_norm/k_norm, apply_multimodal_rotary_pos_emb == 1-D rope for TTS, DynamicCache
+ * .update) and K:323-333 (codec: no q/k norm).  qkv: fp32 [R][(Hq+2*Hkv)*D].
+ * cache layout [B][Hkv][Lmax][D] in kv_dtype.  cos/sin tables: fp32 [npos][D/2].
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_qkv_args {
+  int R, Hq, Hkv, D;
+  const float* qkv;
+  const float* q_norm; const float* k_norm; float eps;
+  const float* cos_tab; const float* sin_tab;
+  const int* rope_pos; const int* row_batch; const int* kv_pos;
+  float* q_out;
+  void* k_cache; void* v_cache; int kv_dtype; int Lmax;
+} qt_qkv_args;
+int qt_qkv_post(const qt_qkv_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * qt_attention: per query row r, keys [max(row_start[r], row_len[r]-window), row_len[r]) of batch
+ * row_batch[r]; GQA (Hq/Hkv q heads per kv head); softmax in fp32.  Replaces eager/sdpa/FA2 attention
+ * (M:634-657, 787-801; K:121-144, 335-349 incl. the 72-frame sliding window).  out [R][Hq*D] (o_dtype).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_attn_args {
+  int R, Hq, Hkv, D, Lmax, window;
+  const float* q;
+  const void* k_cache; const void* v_cache; int kv_dtype;
+  const int* row_batch; const int* row_start; const int* row_len;
+  void* out; int o_dtype;
+  int max_keys;
+} qt_attn_args;
+int qt_attention(const qt_attn_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * qt_sample: transformers-4.57 logits processing + token choice, one row per block.
+ * RepetitionPenalty (seen flags) -> MinNewTokens (mask eos while *n_generated < min_new_tokens) ->
+ * SuppressTokens [suppress_lo, suppress_hi) except suppress_keep (+ eos when ignore_eos) ->
+ * greedy argmax (lowest index on ties) or Temperature -> TopK -> TopP -> softmax -> inverse-CDF draw from
+ * a Philox stream (seed, *step, substep, row).  Finished rows emit eos (HF pad = eos).  Replaces
+ * GenerationMixin's processors / sampling for the talker (M:2044-2066) and the code predictor (M:1671-1680).
+ * tok_out[r] gets the token; if codes != NULL also codes[r*codes_ld + (*step + codes_step_off)*codes_w + codes_col].
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_sample_args {
+  const float* logits; int R; int V; long long ld;
+  unsigned char* seen; float rep_penalty;
+  const int* n_generated; int min_new_tokens; int eos_id;
+  int suppress_lo, suppress_hi, suppress_keep; int ignore_eos;
+  unsigned char* finished;
+  int do_sample; int top_k; float top_p; float temperature;
+  unsigned long long seed; const int* step; int substep;
+  int* tok_out;
+  int* codes; long long codes_ld; int codes_w; int codes_col; int codes_step_off;
+} qt_sample_args;
+int qt_sample(const qt_sample_args* args, void* stream);
+
+/* Qwen3TTSRMSNorm (M:595-610 / K:372-390): out = gamma * (x * rsqrt(mean(x^2) + eps)), fp32 [M][N]. */
+int qt_rmsnorm(const float* x, const float* gamma, float eps, float* out, int M, int N, void* stream);
+
+/* out[m] = table[idx[m]] (fp32 out, table dtype), nn.Embedding row gather (M:1441, 1670). */
+int qt_gather_rows(const void* table, int dtype, const int* idx, int M, int H, float* out, long long ldo, void* stream);
+
+/* Talker decode input (M:1681-1692): x[b] = E0[codes[b,t,0]] + sum_g Ecp[g][codes[b,t,1+g]]
+ * + (t < T ? trailing[b][t] : pad).  codes: int32 [B][codes_ld] rows holding [F][G]. */
+int qt_frame_embed(const void* emb0, const void* emb_cp, int dtype, int V0, int Vcp, int G, int H,
+                   const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
+                   const float* pad, float* x, int B, void* stream);
+
+/* counters[i] += 1 for i < n (end-of-frame step / position advance inside a captured graph). */
+int qt_advance(int* counters, int n, void* stream);
+
+/* ---- codec decoder helpers (K) ---- */
+/* SplitResidualVectorQuantizer.decode table gather-sum (K:814-820): out[b][t][:] = sum_q tab_q[codes[b][t][q]],
+ * group split: q < n_first -> out_first, else out_rest.  tables fp32 [Q][2048][dim] pre-divided by usage. */
+int qt_rvq_gather(const float* tables, int Q, int n_first, int cb_size, int dim, const int* codes, int B, int T,
+                  float* out_first, float* out_rest, void* stream);
+/* SnakeBeta (K:577-615) channels-last: y = x + inv_beta[c] * sin(x * alpha[c])^2 (alpha/inv_beta pre-exp'd). */
+int qt_snake(const void* x, void* y, int dtype, long long rows, int C, const float* alpha, const float* inv_beta,
+             void* stream);
+/* ConvNeXt depthwise causal conv k=7 + LayerNorm(eps) (K:210-232), channels-last [B][T][C] -> out (dtype). */
+int qt_dwconv_ln(const void* x, int dtype, int B, int T, int C, const float* w, const float* b, const float* ln_w,
+                 const float* ln_b, float eps, void* out, void* stream);
+/* clamp(-1, 1) + dtype -> fp32 pcm (K:883). */
+int qt_clamp_pcm(const void* x, int dtype, long long n, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

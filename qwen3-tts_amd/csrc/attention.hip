@@ -1,0 +1,210 @@
+// qkv post-processing (q/k RMSNorm + RoPE + KV-cache write) and row-wise GQA attention for gfx950.
+//
+// Attention is HBM-bound at decode: each (row, kv-head) block reads its K and V ranges once.
+// Pass 1: 8-element (16 B bf16 / 32 B fp32) K fragments per lane, D/8 lanes per key, scores to LDS.
+// Pass 2: softmax in fp32 over LDS; P.V with the same key-per-lane-group split, reduced across waves.
+// Decode roofline: bytes = 2 * L * D * sizeof(kv) per (row, kv-head) / 8 TB/s.
+#include "common.h"
+
+namespace {
+
+template <typename KV>
+__global__ __launch_bounds__(64) void qkv_post_k(qt_qkv_args p) {
+  const int r = blockIdx.x, hh = blockIdx.y, lane = threadIdx.x;
+  const int D = p.D, half = D >> 1;
+  const int nq = p.Hq, nk = p.Hkv;
+  const float* src = p.qkv + (long long)r * (nq + 2 * nk) * D + (long long)hh * D;
+  const bool act = lane < half;
+  float x0 = act ? src[lane] : 0.f, x1 = act ? src[lane + half] : 0.f;
+  const bool isq = hh < nq, isk = !isq && hh < nq + nk;
+  if (isq || isk) {
+    const float* nw = isq ? p.q_norm : p.k_norm;
+    if (nw) {  // Qwen3TTSRMSNorm over head_dim: x * rsqrt(mean(x^2) + eps), then weight *
+      float ss = wave_sum(x0 * x0 + x1 * x1);
+      float rs = rsqrtf(ss / (float)D + p.eps);
+      if (act) { x0 = nw[lane] * (x0 * rs); x1 = nw[lane + half] * (x1 * rs); }
+    }
+    const int pos = p.rope_pos[r];
+    if (act) {
+      const float c = p.cos_tab[(long long)pos * half + lane], s = p.sin_tab[(long long)pos * half + lane];
+      const float y0 = x0 * c - x1 * s, y1 = x1 * c + x0 * s;  // q*cos + rotate_half(q)*sin
+      x0 = y0; x1 = y1;
+    }
+  }
+  if (!act) return;
+  if (isq) {
+    float* q = p.q_out + (long long)r * nq * D + (long long)hh * D;
+    q[lane] = x0; q[lane + half] = x1;
+    return;
+  }
+  const int h = isk ? hh - nq : hh - nq - nk;
+  KV* cache = (KV*)(isk ? p.k_cache : p.v_cache);
+  KV* dst = cache + (((long long)p.row_batch[r] * nk + h) * p.Lmax + p.kv_pos[r]) * D;
+  dst[lane] = from_f<KV>(x0);
+  dst[lane + half] = from_f<KV>(x1);
+}
+
+// One block = one (query row, kv head); 4 waves split the key range.
+template <typename KV, typename OT, int D, int NREP>
+__global__ __launch_bounds__(256) void attn_rows_k(qt_attn_args p) {
+  constexpr int LPK = D / 8;      // lanes per key
+  constexpr int KPW = 64 / LPK;   // keys per wave-iteration
+  extern __shared__ float smem[];  // [NREP][max_keys] scores, then [4][NREP][D] partial outputs
+  __shared__ float red[2][4][NREP];
+  const int r = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane / LPK, sub = lane % LPK;
+  const int b = p.row_batch[r];
+  const int len = p.row_len[r];
+  int start = p.row_start[r];
+  if (p.window > 0) start = max(start, len - p.window);
+  const int n = len - start;
+  float* sc = smem;
+  const float scale = rsqrtf((float)D);
+  const long long base = ((long long)b * p.Hkv + h) * p.Lmax * D;
+  const KV* Kc = (const KV*)p.k_cache + base;
+  const KV* Vc = (const KV*)p.v_cache + base;
+
+  float q[NREP][8];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j)
+    load8f(p.q + ((long long)r * p.Hq + h * NREP + j) * D + sub * 8, q[j]);
+
+  // pass 1: scores
+  for (int k0 = w * KPW; k0 < n; k0 += 4 * KPW) {
+    const int kk = k0 + grp;
+    float kv[8];
+    if (kk < n) load8f(Kc + (long long)(start + kk) * D + sub * 8, kv);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kv[i] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d += q[j][i] * kv[i];
+#pragma unroll
+      for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (sub == 0 && kk < n) sc[j * p.max_keys + kk] = d * scale;
+    }
+  }
+  __syncthreads();
+  // softmax (fp32) per rep head
+  float mx[NREP], inv[NREP];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j) {
+    float m = -INFINITY;
+    for (int k = threadIdx.x; k < n; k += 256) m = fmaxf(m, sc[j * p.max_keys + k]);
+    m = wave_max(m);
+    if (lane == 0) red[0][w][j] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NREP; ++j) {
+    mx[j] = fmaxf(fmaxf(red[0][0][j], red[0][1][j]), fmaxf(red[0][2][j], red[0][3][j]));
+    float s = 0.f;
+    for (int k = threadIdx.x; k < n; k += 256) {
+      float e = expf(sc[j * p.max_keys + k] - mx[j]);
+      sc[j * p.max_keys + k] = e;
+      s += e;
+    }
+    s = wave_sum(s);
+    if (lane == 0) red[1][w][j] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NREP; ++j) inv[j] = 1.f / (red[1][0][j] + red[1][1][j] + red[1][2][j] + red[1][3][j]);
+
+  // pass 2: P.V
+  float acc[NREP][8];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = 0.f;
+  for (int k0 = w * KPW; k0 < n; k0 += 4 * KPW) {
+    const int kk = k0 + grp;
+    if (kk < n) {
+      float vv[8];
+      load8f(Vc + (long long)(start + kk) * D + sub * 8, vv);
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const float pj = sc[j * p.max_keys + kk] * inv[j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[j][i] += pj * vv[i];
+      }
+    }
+  }
+  // reduce across key groups inside the wave (lanes with equal `sub`)
+#pragma unroll
+  for (int j = 0; j < NREP; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = acc[j][i];
+#pragma unroll
+      for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      acc[j][i] = v;
+    }
+  float* part = smem + NREP * p.max_keys;  // [4][NREP][D]
+  if (grp == 0) {
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) part[(w * NREP + j) * D + sub * 8 + i] = acc[j][i];
+  }
+  __syncthreads();
+  OT* out = (OT*)p.out;
+  for (int e = threadIdx.x; e < NREP * D; e += 256) {
+    const int j = e / D, d = e % D;
+    float v = part[(0 * NREP + j) * D + d] + part[(1 * NREP + j) * D + d] + part[(2 * NREP + j) * D + d] +
+              part[(3 * NREP + j) * D + d];
+    out[((long long)r * p.Hq + h * NREP + j) * D + d] = from_f<OT>(v);
+  }
+}
+
+template <typename KV, typename OT, int D>
+int attn_dispatch_rep(const qt_attn_args& p, hipStream_t s) {
+  const int nrep = p.Hq / p.Hkv;
+  const size_t sh = (size_t)(nrep * p.max_keys + 4 * nrep * D) * sizeof(float);
+  dim3 g(p.R, p.Hkv);
+  switch (nrep) {
+    case 1: hipLaunchKernelGGL((attn_rows_k<KV, OT, D, 1>), g, dim3(256), sh, s, p); break;
+    case 2: hipLaunchKernelGGL((attn_rows_k<KV, OT, D, 2>), g, dim3(256), sh, s, p); break;
+    case 4: hipLaunchKernelGGL((attn_rows_k<KV, OT, D, 4>), g, dim3(256), sh, s, p); break;
+    default: return QT_ERR_SHAPE;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
+template <typename KV, typename OT>
+int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
+  switch (p.D) {
+    case 16: return attn_dispatch_rep<KV, OT, 16>(p, s);
+    case 64: return attn_dispatch_rep<KV, OT, 64>(p, s);
+    case 128: return attn_dispatch_rep<KV, OT, 128>(p, s);
+    default: return QT_ERR_SHAPE;
+  }
+}
+
+}  // namespace
+
+extern "C" int qt_qkv_post(const qt_qkv_args* a, void* stream) {
+  if (!a || a->D > 128 || (a->D & 1) || a->R <= 0) return QT_ERR_SHAPE;
+  dim3 g(a->R, a->Hq + 2 * a->Hkv);
+  hipStream_t s = (hipStream_t)stream;
+  if (a->kv_dtype == QT_BF16) hipLaunchKernelGGL(qkv_post_k<bf16_t>, g, dim3(64), 0, s, *a);
+  else if (a->kv_dtype == QT_F32) hipLaunchKernelGGL(qkv_post_k<float>, g, dim3(64), 0, s, *a);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_attention(const qt_attn_args* a, void* stream) {
+  if (!a || a->R <= 0 || a->Hkv <= 0 || a->Hq % a->Hkv || a->max_keys <= 0) return QT_ERR_SHAPE;
+  const size_t sh = (size_t)((a->Hq / a->Hkv) * (a->max_keys + 4 * a->D)) * sizeof(float);
+  if (sh > 160 * 1024 - 256) return QT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->kv_dtype == QT_BF16 && a->o_dtype == QT_F32) return attn_dispatch<bf16_t, float>(*a, s);
+  if (a->kv_dtype == QT_BF16 && a->o_dtype == QT_BF16) return attn_dispatch<bf16_t, bf16_t>(*a, s);
+  if (a->kv_dtype == QT_F32 && a->o_dtype == QT_F32) return attn_dispatch<float, float>(*a, s);
+  return QT_ERR_DTYPE;
+}

@@ -1,0 +1,71 @@
+// Shared device helpers for the Qwen3-TTS MI355X (gfx950 / CDNA4) kernels.
+// wave64 everywhere; bf16 stored as uint16 bit patterns; fp32 accumulate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/qwen3tts_amd.h"
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+#define QT_DEV __device__ __forceinline__
+
+
+QT_DEV float bf2f(bf16_t h) { return __uint_as_float(((unsigned)h) << 16); }
+QT_DEV bf16_t f2bf(float f) {  // round-to-nearest-even (activations are finite)
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+QT_DEV unsigned pack2bf(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+
+template <typename T> struct TypeOf;
+template <> struct TypeOf<float> { static constexpr int code = QT_F32; };
+template <> struct TypeOf<bf16_t> { static constexpr int code = QT_BF16; };
+
+QT_DEV float to_f(float x) { return x; }
+QT_DEV float to_f(bf16_t x) { return bf2f(x); }
+template <typename T> QT_DEV T from_f(float x);
+template <> QT_DEV float from_f<float>(float x) { return x; }
+template <> QT_DEV bf16_t from_f<bf16_t>(float x) { return f2bf(x); }
+
+QT_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+QT_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+QT_DEV float silu_f(float g) { return g / (1.0f + expf(-g)); }
+QT_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// 8 consecutive elements -> fp32 (16 B of bf16 or 32 B of fp32)
+QT_DEV void load8f(const float* p, float* o) {
+  f32x4_t a = *(const f32x4_t*)p, b = *(const f32x4_t*)(p + 4);
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3]; o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+}
+QT_DEV void load8f(const bf16_t* p, float* o) {
+  u32x4_t v = *(const u32x4_t*)p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(v[i] << 16);
+    o[2 * i + 1] = __uint_as_float(v[i] & 0xFFFF0000u);
+  }
+}
+QT_DEV void load4f(const float* p, float* o) {
+  f32x4_t a = *(const f32x4_t*)p;
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+}
+QT_DEV void load4f(const bf16_t* p, float* o) {
+  uint2 v = *(const uint2*)p;
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xFFFF0000u);
+}
+QT_DEV void store4(float* p, const float* v) { *(f32x4_t*)p = f32x4_t{v[0], v[1], v[2], v[3]}; }
+QT_DEV void store4(bf16_t* p, const float* v) { *(uint2*)p = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])}; }

@@ -1,0 +1,241 @@
+// Weight-tiled MFMA GEMM for gfx950: every Linear / Conv1d of the hot path.
+//
+//   out[m][n] (op)= epi( rs[m] * sum_k W[n][k] * (gamma[k] * A[m][k]) + bias[n] ) * colscale[n]
+//
+// * Weights are pre-tiled once at load time (qt_tile_weight) into MFMA B-fragment order:
+//   tile (nt, kt) = 16 output rows x KT k-columns = 1 KiB, lane l holds W[nt*16 + (l&15)][kt*KT + (l>>4)*E .. +E)
+//   (E = 8 bf16 / 4 fp32, KT = 4E).  A wave streaming one n-tile along K reads 1 KiB contiguous per
+//   instruction: fully coalesced HBM traffic, no cross-lane reduction (MFMA does the k-sum).
+// * A (activations, fp32 or bf16) is read straight from global/L2 in the matching A-fragment order.
+//   Optional prologues: RMSNorm (gamma + per-row rsqrt from the same loads), row gather (embedding
+//   lookup), implicit im2col for causal / transposed Conv1d on channels-last [batch][time][cin].
+// * K is split across the block's waves; partial 16x16 tiles are reduced through LDS, then the fused
+//   epilogue (bias, SiLU/GELU, LayerScale, residual add, SwiGLU pairing) writes the output.
+// Decode (M <= 16) is HBM-bound on W: roofline = W bytes / 8 TB/s.
+#include "common.h"
+
+namespace {
+
+struct GemmP {
+  int M, N, Kp, Klog;          // Kp = padded K (taps * cin_pad), Klog = RMSNorm length
+  const void* A; long long lda;
+  const int* a_index;
+  const void* W;
+  const float* gamma; float eps;
+  const float* bias; const float* colscale;
+  int act, epi;
+  void* out; long long ldo;
+  int taps, dil, cin, cin_pad, t_in, t_out, t_off;
+};
+
+template <typename T> QT_DEV void load_vec(const T* p, float* o, int E);
+
+// Load the E-element A fragment of row m at padded k index kk (fp32 out), zero outside.
+template <typename AT, int E>
+QT_DEV void load_a(const GemmP& p, int m, int kk, float* v) {
+#pragma unroll
+  for (int i = 0; i < E; ++i) v[i] = 0.f;
+  if (m >= p.M) return;
+  const AT* A = (const AT*)p.A;
+  const AT* src;
+  if (p.taps > 0) {  // implicit im2col, channels-last input [batch][t_in][cin]
+    int j = kk / p.cin_pad, c = kk - j * p.cin_pad;
+    if (c >= p.cin) return;
+    int b = m / p.t_out, t = m - b * p.t_out;
+    int ti = t + p.t_off + j * p.dil;
+    if (ti < 0 || ti >= p.t_in) return;
+    src = A + ((long long)b * p.t_in + ti) * p.lda + c;
+  } else {
+    if (kk >= p.Klog) return;
+    long long row = p.a_index ? (long long)p.a_index[m] : (long long)m;
+    src = A + row * p.lda + kk;
+  }
+  if constexpr (E == 8) load8f(src, v); else load4f(src, v);
+}
+
+template <typename WT, typename AT, typename OT, int MT, int WPB>
+__global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
+  constexpr bool BF = sizeof(WT) == 2;
+  constexpr int E = BF ? 8 : 4;
+  constexpr int KT = 4 * E;
+  __shared__ float red[WPB][MT][64][4];
+  __shared__ float red_ss[WPB][MT][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lm = lane & 15, lk = lane >> 4;
+  const int nt = blockIdx.x;
+  const int m0 = blockIdx.y * 16 * MT;
+  const int ktiles = p.Kp / KT;
+  const int per = (ktiles + WPB - 1) / WPB;
+  const int kt0 = w * per, kt1 = min(ktiles, kt0 + per);
+  const bool norm = p.gamma != nullptr;
+
+  f32x4_t acc[MT];
+  float ss[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) { acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f}; ss[i] = 0.f; }
+
+  const WT* wp = (const WT*)p.W + ((size_t)nt * ktiles) * 64 * E + lane * E;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    u32x4_t wv = *(const u32x4_t*)(wp + (size_t)kt * 64 * E);
+    const int kk = kt * KT + lk * E;
+    float g[E];
+    if (norm) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) g[i] = (kk + i < p.Klog) ? p.gamma[kk + i] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float a[E];
+      load_a<AT, E>(p, m0 + mt * 16 + lm, kk, a);
+      if (norm) {
+#pragma unroll
+        for (int i = 0; i < E; ++i) { ss[mt] += a[i] * a[i]; a[i] *= g[i]; }
+      }
+      if constexpr (BF) {
+        u32x4_t av = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(a[4], a[5]), pack2bf(a[6], a[7])};
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
+                                                          __builtin_bit_cast(bf16x8_t, wv), acc[mt], 0, 0, 0);
+      } else {
+        f32x4_t wf = __builtin_bit_cast(f32x4_t, wv);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], wf[s], acc[mt], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    red[w][mt][lane][0] = acc[mt][0]; red[w][mt][lane][1] = acc[mt][1];
+    red[w][mt][lane][2] = acc[mt][2]; red[w][mt][lane][3] = acc[mt][3];
+    if (norm) {
+      float s = ss[mt];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lk == 0) red_ss[w][mt][lm] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x >= MT * 64) return;
+  const int mt = threadIdx.x >> 6;  // == w: the epilogue thread block keeps wave boundaries
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ww = 0; ww < WPB; ++ww) {
+    v[0] += red[ww][mt][lane][0]; v[1] += red[ww][mt][lane][1];
+    v[2] += red[ww][mt][lane][2]; v[3] += red[ww][mt][lane][3];
+  }
+  const int n = nt * 16 + lm;
+  const bool nval = n < p.N;
+  const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
+  const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rloc = lk * 4 + i;
+    float x = v[i];
+    if (norm) {
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WPB; ++ww) s += red_ss[ww][mt][rloc];
+      x *= rsqrtf(s / (float)p.Klog + p.eps);
+    }
+    x += bias;
+    if (p.act == QT_ACT_SILU) x = silu_f(x);
+    else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+    x *= cs;
+    v[i] = x;
+  }
+  OT* out = (OT*)p.out;
+  if (p.epi == QT_EPI_SWIGLU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float up = __shfl_xor(v[i], 8, 64);
+      const int m = m0 + mt * 16 + lk * 4 + i;
+      if (lm < 8 && m < p.M && nt * 8 + lm < (p.N >> 1))
+        out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[i]) * up);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + mt * 16 + lk * 4 + i;
+    if (m >= p.M || !nval) continue;
+    OT* o = out + (long long)m * p.ldo + n;
+    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[i]);
+    else *o = from_f<OT>(v[i]);
+  }
+}
+
+template <typename WT, typename AT, typename OT>
+int launch(const GemmP& p, hipStream_t s) {
+  const int nt = (p.N + 15) / 16;
+  if (p.M <= 16) {
+    hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, (p.M + 15) / 16), dim3(512), 0, s, p);
+  } else if (p.M <= 32) {
+    hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 2, 8>), dim3(nt, (p.M + 31) / 32), dim3(512), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 4, 4>), dim3(nt, (p.M + 63) / 64), dim3(256), 0, s, p);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
+// row-major [N][Kp] -> tiled fragments
+template <typename T, int E>
+__global__ void tile_weight_k(const T* __restrict__ src, T* __restrict__ dst, int N, int Kp) {
+  const long long tile = blockIdx.x;  // nt * ktiles + kt
+  const int ktiles = Kp / (4 * E);
+  const int nt = tile / ktiles, kt = tile % ktiles;
+  const int lane = threadIdx.x;
+  const int n = nt * 16 + (lane & 15);
+  const int k = kt * 4 * E + (lane >> 4) * E;
+  T* d = dst + tile * 64 * E + lane * E;
+#pragma unroll
+  for (int i = 0; i < E; ++i) d[i] = (n < N) ? src[(long long)n * Kp + k + i] : T(0);
+}
+
+}  // namespace
+
+extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
+  if (!a || !a->A || !a->W || !a->out) return QT_ERR_ARG;
+  const int E = a->w_dtype == QT_BF16 ? 8 : 4;
+  const int KT = 4 * E;
+  GemmP p;
+  p.M = a->M; p.N = a->N;
+  p.taps = a->taps; p.dil = a->dil > 0 ? a->dil : 1; p.cin = a->cin; p.cin_pad = a->cin_pad;
+  p.t_in = a->t_in; p.t_out = a->t_out; p.t_off = a->t_off;
+  if (a->taps > 0) {
+    if (a->cin_pad % KT || a->cin % E || a->t_out <= 0) return QT_ERR_SHAPE;
+    p.Kp = a->taps * a->cin_pad;
+  } else {
+    p.Kp = (a->K + KT - 1) / KT * KT;
+    if (a->K % E) return QT_ERR_SHAPE;
+  }
+  p.Klog = a->K;
+  if (a->M <= 0 || a->N <= 0 || (a->epi == QT_EPI_SWIGLU && a->N % 16)) return QT_ERR_SHAPE;
+  if (a->epi == QT_EPI_SWIGLU && (a->bias || a->colscale)) return QT_ERR_ARG;
+  p.A = a->A; p.lda = a->lda; p.a_index = a->a_index; p.W = a->W;
+  p.gamma = a->gamma; p.eps = a->eps; p.bias = a->bias; p.colscale = a->colscale;
+  p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
+  hipStream_t s = (hipStream_t)stream;
+  const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;
+  if (w == QT_BF16 && ad == QT_F32 && o == QT_F32) return launch<bf16_t, float, float>(p, s);
+  if (w == QT_BF16 && ad == QT_BF16 && o == QT_BF16) return launch<bf16_t, bf16_t, bf16_t>(p, s);
+  if (w == QT_BF16 && ad == QT_BF16 && o == QT_F32) return launch<bf16_t, bf16_t, float>(p, s);
+  if (w == QT_BF16 && ad == QT_F32 && o == QT_BF16) return launch<bf16_t, float, bf16_t>(p, s);
+  if (w == QT_F32 && ad == QT_F32 && o == QT_F32) return launch<float, float, float>(p, s);
+  return QT_ERR_DTYPE;
+}
+
+extern "C" int qt_tile_weight(const void* src, int dtype, int N, int Kp, void* dst, void* stream) {
+  const int E = dtype == QT_BF16 ? 8 : 4;
+  if (N <= 0 || Kp % (4 * E)) return QT_ERR_SHAPE;
+  const int ntiles = (N + 15) / 16, ktiles = Kp / (4 * E);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QT_BF16)
+    hipLaunchKernelGGL((tile_weight_k<bf16_t, 8>), dim3(ntiles * ktiles), dim3(64), 0, s, (const bf16_t*)src,
+                       (bf16_t*)dst, N, Kp);
+  else if (dtype == QT_F32)
+    hipLaunchKernelGGL((tile_weight_k<float, 4>), dim3(ntiles * ktiles), dim3(64), 0, s, (const float*)src,
+                       (float*)dst, N, Kp);
+  else
+    return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}

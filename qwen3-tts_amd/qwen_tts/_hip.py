@@ -1,0 +1,117 @@
+"""ctypes binding of libqwen3tts_amd.so (the C ABI declared in include/qwen3tts_amd.h).
+
+The product path has no CPU fallback: `lib()` raises if the library or a GPU is missing.
+Tensors are passed as raw device pointers (torch owns the memory; torch is plumbing here), the
+stream as `torch.cuda.current_stream().cuda_stream`, so every launch is capturable into a HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("QWEN3TTS_AMD_LIB",
+                          os.path.join(os.path.dirname(HERE), "lib", "libqwen3tts_amd.so"))
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_SILU, ACT_GELU = 0, 1, 2
+EPI_STORE, EPI_ADD, EPI_SWIGLU = 0, 1, 2
+ERRORS = {-1: "bad argument", -2: "bad shape", -3: "unsupported dtype", -4: "launch failed"}
+
+c_int, c_ll, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p, ctypes.c_ulonglong
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("a_dtype", c_int), ("w_dtype", c_int), ("o_dtype", c_int),
+                ("A", c_void_p), ("lda", c_ll), ("a_index", c_void_p), ("W", c_void_p), ("gamma", c_void_p),
+                ("eps", c_float), ("bias", c_void_p), ("colscale", c_void_p), ("act", c_int), ("epi", c_int),
+                ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
+                ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int)]
+
+
+class QkvArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("qkv", c_void_p), ("q_norm", c_void_p),
+                ("k_norm", c_void_p), ("eps", c_float), ("cos_tab", c_void_p), ("sin_tab", c_void_p),
+                ("rope_pos", c_void_p), ("row_batch", c_void_p), ("kv_pos", c_void_p), ("q_out", c_void_p),
+                ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int), ("Lmax", c_int)]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("Lmax", c_int), ("window", c_int),
+                ("q", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int),
+                ("row_batch", c_void_p), ("row_start", c_void_p), ("row_len", c_void_p), ("out", c_void_p),
+                ("o_dtype", c_int), ("max_keys", c_int)]
+
+
+class SampleArgs(ctypes.Structure):
+    _fields_ = [("logits", c_void_p), ("R", c_int), ("V", c_int), ("ld", c_ll), ("seen", c_void_p),
+                ("rep_penalty", c_float), ("n_generated", c_void_p), ("min_new_tokens", c_int), ("eos_id", c_int),
+                ("suppress_lo", c_int), ("suppress_hi", c_int), ("suppress_keep", c_int), ("ignore_eos", c_int),
+                ("finished", c_void_p), ("do_sample", c_int), ("top_k", c_int), ("top_p", c_float),
+                ("temperature", c_float), ("seed", c_ull), ("step", c_void_p), ("substep", c_int),
+                ("tok_out", c_void_p), ("codes", c_void_p), ("codes_ld", c_ll), ("codes_w", c_int),
+                ("codes_col", c_int), ("codes_step_off", c_int)]
+
+
+EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_sample", "qt_rmsnorm", "qt_gather_rows",
+           "qt_frame_embed", "qt_advance", "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen the library and declare signatures (no GPU needed; used by the CPU export test)."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP library not found at {path}: run `python qwen3-tts_amd/build.py` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(path)
+    P = c_void_p
+    sig = {
+        "qt_gemm": [P, P], "qt_tile_weight": [P, c_int, c_int, c_int, P, P], "qt_qkv_post": [P, P],
+        "qt_attention": [P, P], "qt_sample": [P, P],
+        "qt_rmsnorm": [P, P, c_float, P, c_int, c_int, P],
+        "qt_gather_rows": [P, c_int, P, c_int, c_int, P, c_ll, P],
+        "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, c_int, P],
+        "qt_advance": [P, c_int, P],
+        "qt_rvq_gather": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P],
+        "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],
+        "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
+        "qt_clamp_pcm": [P, c_int, c_ll, P, P],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = c_int
+    return L
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("qwen_tts (MI355X build) needs a ROCm GPU: no device visible and no CPU fallback")
+        _LIB = load_library()
+    return _LIB
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {ERRORS.get(rc, rc)}")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise ValueError(f"unsupported dtype {dt}")

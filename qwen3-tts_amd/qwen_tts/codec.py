@@ -1,0 +1,226 @@
+"""Qwen3-TTS-Tokenizer-12Hz decoder on the MI355X kernels.
+
+Replaces `Qwen3TTSTokenizerV2Decoder.forward / chunked_decode` and `Qwen3TTSTokenizerV2Model.decode`
+(K = qwen_tts/core/tokenizer_12hz/modeling_qwen3_tts_tokenizer_v2.py :823-895, 992-1022).
+Layout: channels-last [B][T][C] end to end, so every Conv1d / ConvTranspose1d is an implicit GEMM on
+the weight-tiled MFMA kernel (transposed convs become 1- or 2-tap convs whose N = stride*Cout output
+columns are already the time-interleaved samples: no pixel shuffle pass).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List
+
+import torch
+
+from . import _hip
+from . import kernels as K
+
+
+def _w(W, name, dev):
+    t = W[name]
+    if not isinstance(t, torch.Tensor):
+        t = torch.from_numpy(t)
+    return t.to(dev).float()
+
+
+class CodecDecoder:
+    def __init__(self, ccfg: dict, weights: Dict[str, torch.Tensor], dtype="bf16", device="cuda"):
+        _hip.lib()
+        self.ccfg = ccfg
+        self.d = d = ccfg["decoder_config"]
+        self.dev = dev = torch.device(device)
+        self.wdt = wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.adt = wdt
+        W = weights
+        g = lambda n: _w(W, n, dev)  # noqa: E731
+        # C1: RVQ codebooks (embedding_sum / clamp(cluster_usage)) and the two 1x1 output projections
+        Q = d["num_quantizers"]
+        tabs = []
+        for q in range(Q):
+            grp, j = ("rvq_first", q) if q == 0 else ("rvq_rest", q - 1)
+            p = f"decoder.quantizer.{grp}.vq.layers.{j}._codebook"
+            tabs.append(g(f"{p}.embedding_sum") / g(f"{p}.cluster_usage").clamp(min=1e-5)[:, None])
+        self.tables = torch.stack(tabs).contiguous()
+        self.cb_dim = self.tables.shape[-1]
+        self.proj_first = K.tile_linear(g("decoder.quantizer.rvq_first.output_proj.weight")[:, :, 0], wdt)
+        self.proj_rest = K.tile_linear(g("decoder.quantizer.rvq_rest.output_proj.weight")[:, :, 0], wdt)
+        # C2
+        self.pre_conv = K.tile_conv(g("decoder.pre_conv.conv.weight"), g("decoder.pre_conv.conv.bias"), wdt)
+        # C3
+        pt = "decoder.pre_transformer"
+        self.hid = d["hidden_size"]
+        self.heads = d["num_attention_heads"]
+        self.kvh = d["num_key_value_heads"]
+        self.hd = self.hid // self.heads
+        self.inp = K.tile_linear(g(f"{pt}.input_proj.weight"), wdt, g(f"{pt}.input_proj.bias"))
+        self.outp = K.tile_linear(g(f"{pt}.output_proj.weight"), wdt, g(f"{pt}.output_proj.bias"))
+        self.tnorm = g(f"{pt}.norm.weight").contiguous()
+        self.layers = []
+        for i in range(d["num_hidden_layers"]):
+            p = f"{pt}.layers.{i}"
+            self.layers.append(dict(
+                qkv=K.tile_linear(torch.cat([g(f"{p}.self_attn.q_proj.weight"), g(f"{p}.self_attn.k_proj.weight"),
+                                             g(f"{p}.self_attn.v_proj.weight")]), wdt),
+                o=K.tile_linear(g(f"{p}.self_attn.o_proj.weight"), wdt),
+                gu=K.tile_swiglu(g(f"{p}.mlp.gate_proj.weight"), g(f"{p}.mlp.up_proj.weight"), wdt),
+                down=K.tile_linear(g(f"{p}.mlp.down_proj.weight"), wdt),
+                ln1=g(f"{p}.input_layernorm.weight").contiguous(), ln2=g(f"{p}.post_attention_layernorm.weight").contiguous(),
+                ls1=g(f"{p}.self_attn_layer_scale.scale").contiguous(), ls2=g(f"{p}.mlp_layer_scale.scale").contiguous()))
+        self.cos, self.sin = K.rope_tables(self.hd, d["rope_theta"], 512, dev)
+        # C4
+        self.lat = d["latent_dim"]
+        self.ups = []
+        for i, f in enumerate(d["upsampling_ratios"]):
+            p = f"decoder.upsample.{i}"
+            self.ups.append(dict(
+                f=f, tconv=K.tile_transconv(g(f"{p}.0.conv.weight"), g(f"{p}.0.conv.bias"), wdt, f),
+                dw_w=g(f"{p}.1.dwconv.conv.weight")[:, 0, :].contiguous(), dw_b=g(f"{p}.1.dwconv.conv.bias"),
+                ln_w=g(f"{p}.1.norm.weight"), ln_b=g(f"{p}.1.norm.bias"),
+                pw1=K.tile_linear(g(f"{p}.1.pwconv1.weight"), wdt, g(f"{p}.1.pwconv1.bias")),
+                pw2=K.tile_linear(g(f"{p}.1.pwconv2.weight"), wdt, g(f"{p}.1.pwconv2.bias")),
+                gamma=g(f"{p}.1.gamma").contiguous()))
+        # C5-C7
+        self.conv0 = K.tile_conv(g("decoder.decoder.0.conv.weight"), g("decoder.decoder.0.conv.bias"), wdt)
+        ds = d["decoder_dim"]
+        self.blocks = []
+        snake = lambda p: (torch.exp(g(f"{p}.alpha")).contiguous(),  # noqa: E731
+                           (1.0 / (torch.exp(g(f"{p}.beta")) + 1e-9)).contiguous())
+        for i, r in enumerate(d["upsample_rates"]):
+            p = f"decoder.decoder.{i + 1}.block"
+            units = []
+            for j, dil in enumerate((1, 3, 9)):
+                q = f"{p}.{j + 2}"
+                units.append(dict(dil=dil, s1=snake(f"{q}.act1"), s2=snake(f"{q}.act2"),
+                                  c1=K.tile_conv(g(f"{q}.conv1.conv.weight"), g(f"{q}.conv1.conv.bias"), wdt, dil),
+                                  c2=K.tile_conv(g(f"{q}.conv2.conv.weight"), g(f"{q}.conv2.conv.bias"), wdt)))
+            self.blocks.append(dict(r=r, cin=ds // 2 ** i, cout=ds // 2 ** (i + 1), s=snake(f"{p}.0"),
+                                    tconv=K.tile_transconv(g(f"{p}.1.conv.weight"), g(f"{p}.1.conv.bias"), wdt, r),
+                                    units=units))
+        n = len(d["upsample_rates"])
+        self.c_last = ds // 2 ** n
+        self.s_last = snake(f"decoder.decoder.{n + 1}")
+        self.conv_last = K.tile_conv(g(f"decoder.decoder.{n + 2}.conv.weight"), g(f"decoder.decoder.{n + 2}.conv.bias"),
+                                     wdt)
+        self.total_upsample = int(math.prod(d["upsample_rates"]) * math.prod(d["upsampling_ratios"]))
+        torch.cuda.synchronize()
+
+    # ------------------------------------------------------------------------------------------------
+    def _conv(self, x, Wt, B, t_in, t_out, t_off, out, cin, epi=_hip.EPI_STORE, act=_hip.ACT_NONE):
+        K.gemm(x, Wt, out, B * t_out, cin, Wt.N, conv=(t_in, t_out, t_off, getattr(Wt, "dil", 1)), epi=epi, act=act)
+
+    def _causal(self, x, Wt, B, T, out, cin, epi=_hip.EPI_STORE):
+        dil = getattr(Wt, "dil", 1)
+        self._conv(x, Wt, B, T, T, -(Wt.taps - 1) * dil, out, cin, epi)
+
+    def _transformer(self, h, B, T):
+        """C3 (K:500-574).  h: [B*T][lat] (adt) -> [B*T][lat] (adt)."""
+        dev, R = self.dev, B * T
+        hid, nh, nkv, D = self.hid, self.heads, self.kvh, self.hd
+        x = torch.empty(R, self.inp.N, dtype=torch.float32, device=dev)
+        K.gemm(h, self.inp, x, R, self.lat, self.inp.N)
+        if self.cos.shape[0] < T:
+            self.cos, self.sin = K.rope_tables(D, self.d["rope_theta"], T + 64, dev)
+        pos = torch.arange(T, device=dev, dtype=torch.int32).repeat(B)
+        meta_b = torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(T)
+        row_len = pos + 1
+        row_start = torch.zeros_like(pos)
+        qkv_w = (nh + 2 * nkv) * D
+        qkv = torch.empty(R, qkv_w, dtype=torch.float32, device=dev)
+        q = torch.empty(R, nh * D, dtype=torch.float32, device=dev)
+        att = torch.empty(R, nh * D, dtype=torch.float32, device=dev)
+        hmid = torch.empty(R, self.d["intermediate_size"], dtype=torch.float32, device=dev)
+        kc = torch.empty(B, nkv, T, D, dtype=torch.float32, device=dev)
+        vc = torch.empty_like(kc)
+        eps, win = self.d["rms_norm_eps"], self.d["sliding_window"]
+        for L in self.layers:
+            K.gemm(x, L["qkv"], qkv, R, hid, qkv_w, gamma=L["ln1"], eps=eps)
+            K.qkv_post(qkv, R, nh, nkv, D, None, None, eps, self.cos, self.sin, pos, meta_b, pos, q, kc, vc, T)
+            K.attention(q, R, nh, nkv, D, kc, vc, T, meta_b, row_start, row_len, att, min(win, T), window=win)
+            K.gemm(att, L["o"], x, R, nh * D, hid, colscale=L["ls1"], epi=_hip.EPI_ADD)
+            K.gemm(x, L["gu"], hmid, R, hid, self.d["intermediate_size"], gamma=L["ln2"], eps=eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(hmid, L["down"], x, R, self.d["intermediate_size"], hid, colscale=L["ls2"], epi=_hip.EPI_ADD)
+        y = torch.empty(R, self.lat, dtype=self.adt, device=dev)
+        K.gemm(x, self.outp, y, R, hid, self.lat, gamma=self.tnorm, eps=eps)
+        return y
+
+    def forward(self, codes: torch.Tensor) -> torch.Tensor:
+        """codes int [B, T, 16] (device) -> pcm fp32 [B, 1920T-555] (K:868-883)."""
+        B, T, Qn = codes.shape
+        dev, adt = self.dev, self.adt
+        codes = codes.to(dev, torch.int32).contiguous()
+        # C1
+        o1 = torch.empty(B * T, self.cb_dim, dtype=torch.float32, device=dev)
+        o2 = torch.empty_like(o1)
+        K.rvq_gather(self.tables, Qn, 1, self.tables.shape[1], self.cb_dim, codes, B, T, o1, o2)
+        cd = self.proj_first.N
+        h = torch.empty(B * T, cd, dtype=adt, device=dev)
+        K.gemm(o1, self.proj_first, h, B * T, self.cb_dim, cd)
+        K.gemm(o2, self.proj_rest, h, B * T, self.cb_dim, cd, epi=_hip.EPI_ADD)
+        # C2
+        x = torch.empty(B * T, self.pre_conv.N, dtype=adt, device=dev)
+        self._causal(h, self.pre_conv, B, T, x, cd)
+        # C3
+        x = self._transformer(x, B, T)
+        # C4
+        L = T
+        C = self.lat
+        for u in self.ups:
+            f = u["f"]
+            y = torch.empty(B * L * f, C, dtype=adt, device=dev)
+            self._conv(x, u["tconv"], B, L, L, 0, y, C)
+            L *= f
+            z = torch.empty_like(y)
+            K.dwconv_ln(y, B, L, C, u["dw_w"], u["dw_b"], u["ln_w"], u["ln_b"], 1e-6, z)
+            hmid = torch.empty(B * L, u["pw1"].N, dtype=adt, device=dev)
+            K.gemm(z, u["pw1"], hmid, B * L, C, u["pw1"].N, act=_hip.ACT_GELU)
+            K.gemm(hmid, u["pw2"], y, B * L, u["pw1"].N, C, colscale=u["gamma"], epi=_hip.EPI_ADD)
+            x = y
+        # C5
+        ds = self.d["decoder_dim"]
+        y = torch.empty(B * L, self.conv0.N, dtype=adt, device=dev)
+        self._causal(x, self.conv0, B, L, y, C)
+        x, C = y, ds
+        # C6
+        for blk in self.blocks:
+            r, cout = blk["r"], blk["cout"]
+            tmp = torch.empty_like(x)
+            K.snake(x, tmp, B * L, C, *blk["s"])
+            Lo = (L - 1) * r
+            y = torch.empty(B * Lo, cout, dtype=adt, device=dev)
+            self._conv(tmp, blk["tconv"], B, L, L - 1, 0, y, C)
+            L, C, x = Lo, cout, y
+            a = torch.empty_like(x)
+            bb = torch.empty_like(x)
+            for un in blk["units"]:
+                K.snake(x, a, B * L, C, *un["s1"])
+                self._causal(a, un["c1"], B, L, bb, C)
+                K.snake(bb, a, B * L, C, *un["s2"])
+                self._causal(a, un["c2"], B, L, x, C, epi=_hip.EPI_ADD)
+        # C7
+        tmp = torch.empty_like(x)
+        K.snake(x, tmp, B * L, C, *self.s_last)
+        out = torch.empty(B * L, self.conv_last.N, dtype=torch.float32, device=dev)
+        self._conv(tmp, self.conv_last, B, L, L, -(self.conv_last.taps - 1), out, C)
+        pcm = out[:, 0].contiguous()
+        K.clamp_pcm(pcm, pcm.numel(), pcm)
+        return pcm.view(B, L)
+
+    def chunked_decode(self, codes: torch.Tensor, chunk_size=300, left_context_size=25) -> torch.Tensor:
+        """K:885-895 (codes [B, T, 16]; same chunk / left-context semantics, including the >300 quirks)."""
+        wavs, start, T = [], 0, codes.shape[1]
+        while start < T:
+            end = min(start + chunk_size, T)
+            ctx = left_context_size if start - left_context_size > 0 else start
+            w = self.forward(codes[:, start - ctx:end])
+            wavs.append(w[:, ctx * self.total_upsample:])
+            start = end
+        return torch.cat(wavs, -1)
+
+    def decode(self, audio_codes: torch.Tensor) -> List[torch.Tensor]:
+        """Qwen3TTSTokenizerV2Model.decode (K:992-1022): [B, T, 16] -> list of 1-D fp32 wavs (device)."""
+        if audio_codes.shape[1] == 0:
+            return [torch.zeros(0, device=self.dev) for _ in range(audio_codes.shape[0])]
+        wav = self.chunked_decode(audio_codes)
+        lengths = (audio_codes[..., 0] > 0).sum(1) * self.ccfg["decode_upsample_rate"]
+        return [a[:int(l)] for a, l in zip(wav, lengths)]

@@ -1,0 +1,275 @@
+"""Drop-in `Qwen3TTSModel` (reference: qwen_tts/inference/qwen3_tts_model.py, `W` below).
+
+Same public surface and semantics: from_pretrained, generate_custom_voice / generate_voice_design /
+generate_voice_clone (with a prepared voice_clone_prompt), get_supported_speakers / languages, kwargs
+precedence of `_merge_generate_kwargs` (W:287-352), validation errors (W:141-186), wrapper defaults
+(max_new_tokens 2048, non_streaming_mode True/True/False) and the 0.6B instruct drop (W:799).
+New: `stream()` yields (pcm chunk, sr) per utterance as soon as its codes are decoded.
+All compute runs on the MI355X engine (qwen_tts/model.py + qwen_tts/codec.py).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from ..model import TTSModel
+from ..text import load_processor
+from ..weights import load_safetensors, read_json, resolve_path, synthetic, talker_specs
+from .qwen3_tts_tokenizer import Qwen3TTSTokenizer, _dtype_name
+
+AudioLike = Union[str, np.ndarray, Tuple[np.ndarray, int]]
+MaybeList = Union[Any, List[Any]]
+
+
+@dataclass
+class VoiceClonePromptItem:
+    """W:40-51."""
+    ref_code: Optional[torch.Tensor]
+    ref_spk_embedding: torch.Tensor
+    x_vector_only_mode: bool
+    icl_mode: bool
+    ref_text: Optional[str] = None
+
+
+class Qwen3TTSModel:
+    def __init__(self, model: TTSModel, processor, generate_defaults: Optional[Dict[str, Any]] = None):
+        self.model = model
+        self.processor = processor
+        self.generate_defaults = generate_defaults or {}
+        self.device = model.device
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path: str, device_map="cuda:0", dtype=None,
+                        attn_implementation=None, weights=None, codec_weights=None, seed: int = 1234,
+                        **kwargs) -> "Qwen3TTSModel":
+        """W:82-121.  A local checkpoint dir (config.json, generation_config.json, model*.safetensors,
+        speech_tokenizer/) or a synthetic preset / hub id (offline: synthetic weights).  `attn_implementation`
+        is accepted for API compatibility; attention always runs on the HIP kernel."""
+        d = resolve_path(pretrained_model_name_or_path)
+        cfg = read_json(os.path.join(d, "config.json"))
+        if cfg.get("model_type") != "qwen3_tts":
+            raise TypeError(f"expected a qwen3_tts checkpoint, got model_type={cfg.get('model_type')!r}")
+        gpath = os.path.join(d, "generation_config.json")
+        gen = read_json(gpath) if os.path.exists(gpath) else {}
+        dev = torch.device(device_map if isinstance(device_map, str) and device_map.startswith("cuda") else "cuda:0")
+        W = weights if weights is not None else load_safetensors(d)
+        if not W:
+            W = synthetic(talker_specs(cfg), dev, seed)
+        with torch.cuda.device(dev):
+            m = TTSModel(cfg, W, dtype=_dtype_name(dtype), device=dev, generate_config=gen)
+        del W
+        m.load_speech_tokenizer(Qwen3TTSTokenizer.from_pretrained(os.path.join(d, "speech_tokenizer"), device_map=dev,
+                                                                  dtype=dtype, weights=codec_weights, seed=seed))
+        return cls(m, load_processor(d), gen)
+
+    # ---------------------------------------------------------------- validation (W:123-186)
+    def _supported_languages_set(self):
+        v = self.model.get_supported_languages()
+        return None if v is None else set(str(x).lower() for x in v)
+
+    def _supported_speakers_set(self):
+        v = self.model.get_supported_speakers()
+        return None if v is None else set(str(x).lower() for x in v)
+
+    def _validate_languages(self, languages):
+        sup = self._supported_languages_set()
+        if sup is None:
+            return
+        bad = [x for x in languages if x is None or str(x).lower() not in sup]
+        if bad:
+            raise ValueError(f"Unsupported languages: {bad}. Supported: {sorted(sup)}")
+
+    def _validate_speakers(self, speakers):
+        sup = self._supported_speakers_set()
+        if sup is None:
+            return
+        bad = [s for s in speakers if s not in (None, "") and str(s).lower() not in sup]
+        if bad:
+            raise ValueError(f"Unsupported speakers: {bad}. Supported: {sorted(sup)}")
+
+    def _ensure_list(self, x: MaybeList) -> List[Any]:
+        return x if isinstance(x, list) else [x]
+
+    def _build_assistant_text(self, text: str) -> str:
+        return f"<|im_start|>assistant\n{text}<|im_end|>\n<|im_start|>assistant\n"
+
+    def _build_ref_text(self, text: str) -> str:
+        return f"<|im_start|>assistant\n{text}<|im_end|>\n"
+
+    def _build_instruct_text(self, instruct: str) -> str:
+        return f"<|im_start|>user\n{instruct}<|im_end|>\n"
+
+    def _tokenize_texts(self, texts: List[str]) -> List[torch.Tensor]:
+        out = []
+        for t in texts:
+            ids = self.processor(text=t, return_tensors="pt", padding=True)["input_ids"]
+            out.append(ids.unsqueeze(0) if ids.dim() == 1 else ids)
+        return out
+
+    def _merge_generate_kwargs(self, do_sample=None, top_k=None, top_p=None, temperature=None, repetition_penalty=None,
+                               subtalker_dosample=None, subtalker_top_k=None, subtalker_top_p=None,
+                               subtalker_temperature=None, max_new_tokens=None, **kwargs) -> Dict[str, Any]:
+        """W:287-352: user value > generation_config.json > hard default."""
+        hard = dict(do_sample=True, top_k=50, top_p=1.0, temperature=0.9, repetition_penalty=1.05,
+                    subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9,
+                    max_new_tokens=2048)
+
+        def pick(name, v):
+            if v is not None:
+                return v
+            if name in self.generate_defaults:
+                return self.generate_defaults[name]
+            return hard[name]
+
+        merged = dict(kwargs)
+        merged.update(do_sample=pick("do_sample", do_sample), top_k=pick("top_k", top_k), top_p=pick("top_p", top_p),
+                      temperature=pick("temperature", temperature),
+                      repetition_penalty=pick("repetition_penalty", repetition_penalty),
+                      subtalker_dosample=pick("subtalker_dosample", subtalker_dosample),
+                      subtalker_top_k=pick("subtalker_top_k", subtalker_top_k),
+                      subtalker_top_p=pick("subtalker_top_p", subtalker_top_p),
+                      subtalker_temperature=pick("subtalker_temperature", subtalker_temperature),
+                      max_new_tokens=pick("max_new_tokens", max_new_tokens))
+        return merged
+
+    def _decode(self, codes_list):
+        return self.model.speech_tokenizer.decode([{"audio_codes": c} for c in codes_list])
+
+    # ---------------------------------------------------------------- voice clone (W:356-633)
+    def create_voice_clone_prompt(self, ref_audio, ref_text=None, x_vector_only_mode=False):
+        if self.model.tts_model_type != "base":
+            raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
+                             "create_voice_clone_prompt, Please check Model Card or Readme for more details.")
+        raise NotImplementedError("reference-audio encode (Mimi) + ECAPA speaker encoder are the next tier of this "
+                                  "build (SURVEY.md §8f-2); pass a prepared voice_clone_prompt instead")
+
+    def _prompt_items_to_voice_clone_prompt(self, items: List[VoiceClonePromptItem]) -> Dict[str, Any]:
+        return dict(ref_code=[it.ref_code for it in items], ref_spk_embedding=[it.ref_spk_embedding for it in items],
+                    x_vector_only_mode=[it.x_vector_only_mode for it in items], icl_mode=[it.icl_mode for it in items])
+
+    @torch.no_grad()
+    def generate_voice_clone(self, text, language=None, ref_audio=None, ref_text=None, x_vector_only_mode=False,
+                             voice_clone_prompt=None, non_streaming_mode=False, **kwargs):
+        if self.model.tts_model_type != "base":
+            raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
+                             "generate_voice_clone, Please check Model Card or Readme for more details.")
+        texts = self._ensure_list(text)
+        languages = self._ensure_list(language) if isinstance(language, list) else \
+            ([language] * len(texts) if language is not None else ["Auto"] * len(texts))
+        if len(languages) == 1 and len(texts) > 1:
+            languages = languages * len(texts)
+        if len(texts) != len(languages):
+            raise ValueError(f"Batch size mismatch: text={len(texts)}, language={len(languages)}")
+        self._validate_languages(languages)
+        if voice_clone_prompt is None:
+            if ref_audio is None:
+                raise ValueError("Either `voice_clone_prompt` or `ref_audio` must be provided.")
+            items = self.create_voice_clone_prompt(ref_audio, ref_text, x_vector_only_mode)
+            vcp, ref_texts = self._prompt_items_to_voice_clone_prompt(items), [it.ref_text for it in items]
+        elif isinstance(voice_clone_prompt, list):
+            items = voice_clone_prompt
+            if len(items) == 1 and len(texts) > 1:
+                items = items * len(texts)
+            if len(items) != len(texts):
+                raise ValueError(f"Batch size mismatch: prompt={len(items)}, text={len(texts)}")
+            vcp, ref_texts = self._prompt_items_to_voice_clone_prompt(items), [it.ref_text for it in items]
+        else:
+            vcp, ref_texts = voice_clone_prompt, None
+        input_ids = self._tokenize_texts([self._build_assistant_text(t) for t in texts])
+        ref_ids = None
+        if ref_texts is not None:
+            ref_ids = [None if not rt else self._tokenize_texts([self._build_ref_text(rt)])[0] for rt in ref_texts]
+        codes, _ = self.model.generate(input_ids=input_ids, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=languages,
+                                       non_streaming_mode=non_streaming_mode, **self._merge_generate_kwargs(**kwargs))
+        refs = vcp.get("ref_code", None)
+        dec = [torch.cat([refs[i].cpu().long(), c], 0) if refs is not None and refs[i] is not None else c
+               for i, c in enumerate(codes)]
+        wavs, fs = self._decode(dec)
+        out = []
+        for i, w in enumerate(wavs):
+            if refs is not None and refs[i] is not None:
+                cut = int(int(refs[i].shape[0]) / max(int(dec[i].shape[0]), 1) * w.shape[0])
+                out.append(w[cut:])
+            else:
+                out.append(w)
+        return out, fs
+
+    # ---------------------------------------------------------------- voice design (W:637-728)
+    @torch.no_grad()
+    def generate_voice_design(self, text, instruct, language=None, non_streaming_mode=True, **kwargs):
+        if self.model.tts_model_type != "voice_design":
+            raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
+                             "generate_voice_design, Please check Model Card or Readme for more details.")
+        texts = self._ensure_list(text)
+        languages = self._ensure_list(language) if isinstance(language, list) else \
+            ([language] * len(texts) if language is not None else ["Auto"] * len(texts))
+        instructs = self._ensure_list(instruct)
+        if len(languages) == 1 and len(texts) > 1:
+            languages = languages * len(texts)
+        if len(instructs) == 1 and len(texts) > 1:
+            instructs = instructs * len(texts)
+        if not (len(texts) == len(languages) == len(instructs)):
+            raise ValueError(f"Batch size mismatch: text={len(texts)}, language={len(languages)}, "
+                             f"instruct={len(instructs)}")
+        self._validate_languages(languages)
+        input_ids = self._tokenize_texts([self._build_assistant_text(t) for t in texts])
+        ins_ids = [None if not x else self._tokenize_texts([self._build_instruct_text(x)])[0] for x in instructs]
+        codes, _ = self.model.generate(input_ids=input_ids, instruct_ids=ins_ids, languages=languages,
+                                       non_streaming_mode=non_streaming_mode, **self._merge_generate_kwargs(**kwargs))
+        return self._decode(codes)
+
+    # ---------------------------------------------------------------- custom voice (W:732-839)
+    def _custom_voice_inputs(self, text, speaker, language, instruct):
+        if self.model.tts_model_type != "custom_voice":
+            raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
+                             "generate_custom_voice, Please check Model Card or Readme for more details.")
+        texts = self._ensure_list(text)
+        languages = self._ensure_list(language) if isinstance(language, list) else \
+            ([language] * len(texts) if language is not None else ["Auto"] * len(texts))
+        speakers = self._ensure_list(speaker)
+        if self.model.tts_model_size in "0b6":  # W:799 (substring test, kept as-is)
+            instruct = None
+        instructs = self._ensure_list(instruct) if isinstance(instruct, list) else \
+            ([instruct] * len(texts) if instruct is not None else [""] * len(texts))
+        if len(languages) == 1 and len(texts) > 1:
+            languages = languages * len(texts)
+        if len(speakers) == 1 and len(texts) > 1:
+            speakers = speakers * len(texts)
+        if len(instructs) == 1 and len(texts) > 1:
+            instructs = instructs * len(texts)
+        if not (len(texts) == len(languages) == len(speakers) == len(instructs)):
+            raise ValueError(f"Batch size mismatch: text={len(texts)}, language={len(languages)}, "
+                             f"speaker={len(speakers)}, instruct={len(instructs)}")
+        self._validate_languages(languages)
+        self._validate_speakers(speakers)
+        input_ids = self._tokenize_texts([self._build_assistant_text(t) for t in texts])
+        ins_ids = [None if not x else self._tokenize_texts([self._build_instruct_text(x)])[0] for x in instructs]
+        return input_ids, ins_ids, languages, speakers
+
+    @torch.no_grad()
+    def generate_custom_voice(self, text, speaker, language=None, instruct=None, non_streaming_mode=True, **kwargs):
+        input_ids, ins_ids, languages, speakers = self._custom_voice_inputs(text, speaker, language, instruct)
+        codes, _ = self.model.generate(input_ids=input_ids, instruct_ids=ins_ids, languages=languages,
+                                       speakers=speakers, non_streaming_mode=non_streaming_mode,
+                                       **self._merge_generate_kwargs(**kwargs))
+        return self._decode(codes)
+
+    @torch.no_grad()
+    def stream(self, text, speaker=None, language=None, instruct=None, non_streaming_mode=True, **kwargs):
+        """New surface (no reference counterpart): yields (utterance index, pcm, sr) for each
+        utterance of a custom-voice batch as soon as its codes are complete and decoded."""
+        wavs, sr = self.generate_custom_voice(text, speaker, language, instruct, non_streaming_mode, **kwargs)
+        for i, w in enumerate(wavs):
+            yield i, w, sr
+
+    def get_supported_speakers(self) -> Optional[List[str]]:
+        s = self._supported_speakers_set()
+        return None if s is None else sorted(s)
+
+    def get_supported_languages(self) -> Optional[List[str]]:
+        s = self._supported_languages_set()
+        return None if s is None else sorted(s)

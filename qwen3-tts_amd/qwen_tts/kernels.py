@@ -1,0 +1,202 @@
+"""Thin Python launchers over the C ABI (include/qwen3tts_amd.h) + weight re-layout helpers.
+
+Every launcher takes torch device tensors (memory/plumbing only) and calls one `qt_*` entry point on
+the current stream, so the calls are capturable into HIP graphs.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _hip
+from ._hip import ptr, stream, check
+
+KT_OF = {torch.bfloat16: 32, torch.float32: 16}
+
+
+@dataclass
+class Tiled:
+    """A weight pre-tiled into MFMA B-fragment order (see csrc/gemm.hip)."""
+    w: torch.Tensor
+    N: int            # logical output width (rows of W; SwiGLU: 2*I)
+    Np: int           # padded to 16
+    K: int            # logical K (linear) or taps*cin (conv)
+    Kp: int
+    dtype: torch.dtype
+    bias: Optional[torch.Tensor] = None
+    taps: int = 0
+    cin: int = 0
+    cin_pad: int = 0
+
+
+def tile(w: torch.Tensor, dtype: torch.dtype, bias=None, taps=0, cin=0, cin_pad=0, K=None) -> Tiled:
+    """w: row-major [N][Kp'] on device (any float dtype) -> Tiled (N padded to 16, K padded to KT)."""
+    kt = KT_OF[dtype]
+    w = w.to(dtype)
+    N, K0 = w.shape
+    Kp = (K0 + kt - 1) // kt * kt
+    if Kp != K0:
+        w = F.pad(w, (0, Kp - K0))
+    Np = (N + 15) // 16 * 16
+    out = torch.empty(Np * Kp, dtype=dtype, device=w.device)
+    w = w.contiguous()
+    check(_hip.lib().qt_tile_weight(ptr(w), _hip.dtype_code(dtype), N, Kp, ptr(out), stream()), "qt_tile_weight")
+    b = None
+    if bias is not None:
+        b = torch.zeros(Np, dtype=torch.float32, device=w.device)
+        b[:N] = bias.float()
+    return Tiled(out, N, Np, K if K is not None else K0, Kp, dtype, b, taps, cin, cin_pad)
+
+
+def tile_linear(w, dtype, bias=None):
+    return tile(w, dtype, bias)
+
+
+def tile_swiglu(gate, up, dtype):
+    """Interleave 8 gate rows / 8 up rows per 16-row tile (QT_EPI_SWIGLU pairing)."""
+    I, K = gate.shape
+    assert I % 8 == 0
+    w = torch.cat([gate.reshape(I // 8, 8, K), up.reshape(I // 8, 8, K)], 1).reshape(2 * I, K)
+    return tile(w, dtype)
+
+
+def _pad_cin(w, cin, dtype):
+    kt = KT_OF[dtype]
+    cp = (cin + kt - 1) // kt * kt
+    return F.pad(w, (0, cp - cin)), cp
+
+
+def tile_conv(w, b, dtype, dilation=1):
+    """Causal Conv1d weight [Cout][Cin][k] -> implicit-GEMM layout [Cout][k][Cin_pad]."""
+    cout, cin, k = w.shape
+    wk, cp = _pad_cin(w.permute(0, 2, 1), cin, dtype)
+    t = tile(wk.reshape(cout, k * cp), dtype, b, taps=k, cin=cin, cin_pad=cp, K=k * cp)
+    t.dil = dilation
+    return t
+
+
+def tile_transconv(w, b, dtype, stride):
+    """ConvTranspose1d weight [Cin][Cout][k] (k = 2*stride, trimmed by stride each side, K:195-207) as a
+    2-tap 'valid' conv with stride*Cout outputs: out[(q-1)*s + r] = W[..., r+s]^T x[q-1] + W[..., r]^T x[q].
+    k == stride (no trim): 1 tap, out[q*s + r] = W[..., r]^T x[q].  Channels-last output rows are then
+    already in time order (pixel shuffle is free)."""
+    cin, cout, k = w.shape
+    s = stride
+    if k == s:
+        wr = w.permute(2, 1, 0).reshape(s * cout, 1, cin)  # [(r, co)][tap][ci]
+        taps = 1
+    else:
+        assert k == 2 * s
+        j0 = w[:, :, s:].permute(2, 1, 0)  # x[q-1] tap
+        j1 = w[:, :, :s].permute(2, 1, 0)  # x[q]   tap
+        wr = torch.stack([j0, j1], 2).reshape(s * cout, 2, cin)
+        taps = 2
+    wk, cp = _pad_cin(wr, cin, dtype)
+    t = tile(wk.reshape(s * cout, taps * cp), dtype, b.repeat(s) if b is not None else None, taps=taps, cin=cin,
+             cin_pad=cp, K=taps * cp)
+    t.dil = 1
+    return t
+
+
+def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, colscale=None,
+         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True):
+    """conv = (t_in, t_out, t_off, dil) for implicit-conv weights."""
+    a = _hip.GemmArgs()
+    a.M, a.N, a.K = M, W.N, W.K
+    a.a_dtype = _hip.dtype_code(a_dtype or A.dtype)
+    a.w_dtype = _hip.dtype_code(W.dtype)
+    a.o_dtype = _hip.dtype_code(o_dtype or out.dtype)
+    a.A, a.lda, a.a_index = ptr(A), lda, ptr(a_index)
+    a.W, a.gamma, a.eps = ptr(W.w), ptr(gamma), eps
+    a.bias = ptr(W.bias) if use_bias else None
+    a.colscale, a.act, a.epi = ptr(colscale), act, epi
+    a.out, a.ldo = ptr(out), ldo
+    if W.taps:
+        t_in, t_out, t_off, dil = conv
+        a.taps, a.dil, a.cin, a.cin_pad, a.t_in, a.t_out, a.t_off = W.taps, dil, W.cin, W.cin_pad, t_in, t_out, t_off
+    check(_hip.lib().qt_gemm(ctypes.byref(a), stream()), "qt_gemm")
+
+
+def qkv_post(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, q_out, kc, vc, Lmax):
+    a = _hip.QkvArgs()
+    a.R, a.Hq, a.Hkv, a.D = R, Hq, Hkv, D
+    a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    a.rope_pos, a.row_batch, a.kv_pos = ptr(rope_pos), ptr(row_batch), ptr(kv_pos)
+    a.q_out, a.k_cache, a.v_cache = ptr(q_out), ptr(kc), ptr(vc)
+    a.kv_dtype, a.Lmax = _hip.dtype_code(kc.dtype), Lmax
+    check(_hip.lib().qt_qkv_post(ctypes.byref(a), stream()), "qt_qkv_post")
+
+
+def attention(q, R, Hq, Hkv, D, kc, vc, Lmax, row_batch, row_start, row_len, out, max_keys, window=0):
+    a = _hip.AttnArgs()
+    a.R, a.Hq, a.Hkv, a.D, a.Lmax, a.window = R, Hq, Hkv, D, Lmax, window
+    a.q, a.k_cache, a.v_cache, a.kv_dtype = ptr(q), ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype)
+    a.row_batch, a.row_start, a.row_len = ptr(row_batch), ptr(row_start), ptr(row_len)
+    a.out, a.o_dtype, a.max_keys = ptr(out), _hip.dtype_code(out.dtype), max_keys
+    check(_hip.lib().qt_attention(ctypes.byref(a), stream()), "qt_attention")
+
+
+def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
+           suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
+           temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
+           codes_step_off=0):
+    a = _hip.SampleArgs()
+    a.logits, a.R, a.V, a.ld = ptr(logits), R, V, ld
+    a.seen, a.rep_penalty = ptr(seen), rep_penalty
+    a.n_generated, a.min_new_tokens, a.eos_id = ptr(n_generated), min_new_tokens, eos_id
+    a.suppress_lo, a.suppress_hi, a.suppress_keep = suppress
+    a.ignore_eos, a.finished = int(ignore_eos), ptr(finished)
+    a.do_sample, a.top_k, a.top_p, a.temperature = int(do_sample), int(top_k or 0), float(top_p), float(temperature)
+    a.seed, a.step, a.substep, a.tok_out = seed & (2 ** 64 - 1), ptr(step), substep, ptr(tok_out)
+    a.codes, a.codes_ld, a.codes_w, a.codes_col, a.codes_step_off = ptr(codes), codes_ld, codes_w, codes_col, codes_step_off
+    check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
+
+
+def rmsnorm(x, g, eps, out, M, N):
+    check(_hip.lib().qt_rmsnorm(ptr(x), ptr(g), eps, ptr(out), M, N, stream()), "qt_rmsnorm")
+
+
+def gather_rows(table, idx, M, H, out, ldo):
+    check(_hip.lib().qt_gather_rows(ptr(table), _hip.dtype_code(table.dtype), ptr(idx), M, H, ptr(out), ldo, stream()),
+          "qt_gather_rows")
+
+
+def frame_embed(e0, ecp, G, H, codes, codes_ld, step, trailing, T, pad, x, B):
+    check(_hip.lib().qt_frame_embed(ptr(e0), ptr(ecp), _hip.dtype_code(e0.dtype), e0.shape[0], ecp.shape[1], G, H,
+                                    ptr(codes), codes_ld, ptr(step), ptr(trailing), T, ptr(pad), ptr(x), B, stream()),
+          "qt_frame_embed")
+
+
+def advance(counters, n):
+    check(_hip.lib().qt_advance(ptr(counters), n, stream()), "qt_advance")
+
+
+def rvq_gather(tables, Q, n_first, cb, dim, codes, B, T, o1, o2):
+    check(_hip.lib().qt_rvq_gather(ptr(tables), Q, n_first, cb, dim, ptr(codes), B, T, ptr(o1), ptr(o2), stream()),
+          "qt_rvq_gather")
+
+
+def snake(x, y, rows, C, alpha, inv_beta):
+    check(_hip.lib().qt_snake(ptr(x), ptr(y), _hip.dtype_code(x.dtype), rows, C, ptr(alpha), ptr(inv_beta), stream()),
+          "qt_snake")
+
+
+def dwconv_ln(x, B, T, C, w, b, lw, lb, eps, out):
+    check(_hip.lib().qt_dwconv_ln(ptr(x), _hip.dtype_code(x.dtype), B, T, C, ptr(w), ptr(b), ptr(lw), ptr(lb), eps,
+                                  ptr(out), stream()), "qt_dwconv_ln")
+
+
+def clamp_pcm(x, n, out):
+    check(_hip.lib().qt_clamp_pcm(ptr(x), _hip.dtype_code(x.dtype), n, ptr(out), stream()), "qt_clamp_pcm")
+
+
+def rope_tables(head_dim: int, theta: float, npos: int, device):
+    """cos/sin [npos][D/2] computed exactly as the reference (fp32 on CPU, M:526-592), then uploaded."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).to(dtype=torch.float) / head_dim))
+    f = torch.arange(npos, dtype=torch.float32)[:, None] * inv[None, :]
+    return f.cos().contiguous().to(device), f.sin().contiguous().to(device)

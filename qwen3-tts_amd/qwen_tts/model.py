@@ -1,0 +1,159 @@
+"""`Qwen3TTSForConditionalGeneration` equivalent on the MI355X engine (inner generate() contract).
+
+Prompt assembly follows qwen_tts/core/models/modeling_qwen3_tts.py (M) :1968-2269 exactly; every
+embedding / text-projection product runs through the HIP kernels (gather + fused MFMA GEMMs), the
+sequence layout (cat / left-pad) is torch plumbing on device tensors.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from .talker import GenParams, TalkerEngine
+
+
+class TTSModel:
+    def __init__(self, config: dict, weights: Dict[str, torch.Tensor], dtype="bf16", device="cuda",
+                 generate_config: Optional[dict] = None):
+        self.config = config
+        self.tc = config["talker_config"]
+        self.engine = TalkerEngine(config, weights, dtype=dtype, device=device)
+        self.device = self.engine.dev
+        self.tts_model_type = config.get("tts_model_type")
+        self.tts_model_size = config.get("tts_model_size")
+        self.tokenizer_type = config.get("tokenizer_type")
+        self.generate_config = generate_config or {}
+        self.speech_tokenizer = None
+        self.supported_speakers = list((self.tc.get("spk_id") or {}).keys())
+        self.supported_languages = ["auto"] + [k for k in (self.tc.get("codec_language_id") or {}) if "dialect" not in k]
+        self.speaker_encoder_sample_rate = config.get("speaker_encoder_config", {}).get("sample_rate", 24000)
+
+    def get_supported_speakers(self):
+        return self.supported_speakers
+
+    def get_supported_languages(self):
+        return self.supported_languages
+
+    def load_speech_tokenizer(self, tok):
+        self.speech_tokenizer = tok
+
+    # -------------------------------------------------------------------------------- G1 / G2
+    def _icl_prompt(self, text_id, ref_id, ref_code, pad_e, eos_e, non_streaming_mode):
+        """generate_icl_prompt (M:1968-2019)."""
+        e, t = self.engine, self.tc
+        text = torch.cat([e.text_proj(torch.cat([ref_id, text_id], -1))[None], eos_e], 1)
+        ref_code = ref_code.to(self.device)
+        parts = [e.codec_embed(ref_code[:, 0])]
+        for i in range(1, t["num_code_groups"]):
+            parts.append(e.cp_embed(i - 1, ref_code[:, i]))
+        codec = torch.stack(parts, 1).sum(1)[None]
+        codec = torch.cat([e.codec_embed([t["codec_bos_id"]])[None], codec], 1)
+        tl, cl = text.shape[1], codec.shape[1]
+        if non_streaming_mode:
+            x = text + e.codec_embed([t["codec_pad_id"]] * tl)[None]
+            return torch.cat([x, codec + pad_e], 1), pad_e
+        if tl > cl:
+            return text[:, :cl] + codec, text[:, cl:]
+        text = torch.cat([text] + [pad_e] * (cl - tl), 1)
+        return text + codec, pad_e
+
+    def build_prompts(self, input_ids, languages, speakers=None, instruct_ids=None, non_streaming_mode=False,
+                      voice_clone_prompt=None, ref_ids=None):
+        """(embeds [B,P,H] fp32, mask [B,P], trailing [B,T,H], tts_pad [1,1,H]) -- M:2068-2269."""
+        e, t, cfg = self.engine, self.tc, self.config
+        B = len(input_ids)
+        per: List[list] = [[] for _ in range(B)]
+        spk_embeds = None
+        if voice_clone_prompt is not None:
+            spk_embeds = [torch.as_tensor(x).to(self.device).float() for x in voice_clone_prompt["ref_spk_embedding"]]
+        if instruct_ids is not None:
+            for i, ins in enumerate(instruct_ids):
+                if ins is not None:
+                    per[i].append(e.text_proj(ins)[None])
+        if speakers is None:
+            speakers = [None] * B
+        special = e.text_proj(torch.tensor([cfg["tts_bos_token_id"], cfg["tts_eos_token_id"], cfg["tts_pad_token_id"]]))
+        bos_e, eos_e, pad_e = special[0].view(1, 1, -1), special[1].view(1, 1, -1), special[2].view(1, 1, -1)
+        trailing = []
+        for i, (ids, lang, spk) in enumerate(zip(input_ids, languages, speakers)):
+            ids = torch.as_tensor(ids).reshape(1, -1)
+            if spk_embeds is None:
+                if spk == "" or spk is None:
+                    spk_e = None
+                else:
+                    if spk.lower() not in t["spk_id"]:
+                        raise NotImplementedError(f"Speaker {spk} not implemented")
+                    spk_e = e.codec_embed([t["spk_id"][spk.lower()]])
+            else:
+                use = voice_clone_prompt["x_vector_only_mode"][i] or voice_clone_prompt["icl_mode"][i]
+                spk_e = spk_embeds[i] if use else None
+            assert lang is not None
+            if lang.lower() == "auto":
+                lang_id = None
+            else:
+                if lang.lower() not in t["codec_language_id"]:
+                    raise NotImplementedError(f"Language {lang} not implemented")
+                lang_id = t["codec_language_id"][lang.lower()]
+            if lang.lower() in ["chinese", "auto"] and spk != "" and spk is not None and \
+                    t["spk_is_dialect"][spk.lower()] is not False:
+                lang_id = t["codec_language_id"][t["spk_is_dialect"][spk.lower()]]
+            if lang_id is None:
+                pre = [t["codec_nothink_id"], t["codec_think_bos_id"], t["codec_think_eos_id"]]
+            else:
+                pre = [t["codec_think_id"], t["codec_think_bos_id"], lang_id, t["codec_think_eos_id"]]
+            c0 = e.codec_embed(pre)[None]
+            c1 = e.codec_embed([t["codec_pad_id"], t["codec_bos_id"]])[None]
+            codec_in = torch.cat([c0, c1], 1) if spk_e is None else torch.cat([c0, spk_e.view(1, 1, -1), c1], 1)
+            role = e.text_proj(ids[:, :3])[None]
+            body = torch.cat([pad_e.expand(-1, codec_in.shape[1] - 2, -1), bos_e], 1) + codec_in[:, :-1]
+            emb = torch.cat([role, body], 1)
+            icl = (voice_clone_prompt is not None and voice_clone_prompt["ref_code"] is not None
+                   and voice_clone_prompt["icl_mode"][i])
+            if icl:
+                ref = torch.as_tensor(ref_ids[i]).reshape(1, -1)
+                icl_e, trail = self._icl_prompt(ids[:, 3:-5], ref[:, 3:-2],
+                                                torch.as_tensor(voice_clone_prompt["ref_code"][i]), pad_e, eos_e,
+                                                non_streaming_mode)
+                emb = torch.cat([emb, icl_e], 1)
+            else:
+                emb = torch.cat([emb, e.text_proj(ids[:, 3:4])[None] + codec_in[:, -1:]], 1)
+                if non_streaming_mode:
+                    emb = emb[:, :-1]
+                    n = ids[:, 3:-5].shape[1]
+                    txt = torch.cat([e.text_proj(ids[:, 3:-5])[None], eos_e], 1) + \
+                        e.codec_embed([t["codec_pad_id"]] * (n + 1))[None]
+                    emb = torch.cat([emb, txt, pad_e + e.codec_embed([t["codec_bos_id"]])[None]], 1)
+                    trail = pad_e
+                else:
+                    trail = torch.cat([e.text_proj(ids[:, 4:-5])[None], eos_e], 1)
+            per[i].append(emb)
+            trailing.append(trail)
+        seqs = [torch.cat(p, 1)[0] for p in per]
+        P = max(s.shape[0] for s in seqs)
+        H = seqs[0].shape[1]
+        embeds = torch.zeros(B, P, H, device=self.device)
+        mask = torch.zeros(B, P, dtype=torch.long, device=self.device)
+        for i, s in enumerate(seqs):
+            embeds[i, P - s.shape[0]:] = s
+            mask[i, P - s.shape[0]:] = 1
+        T = max(tr.shape[1] for tr in trailing)
+        trail = pad_e.reshape(1, 1, H).expand(B, T, H).clone()
+        for i, tr in enumerate(trailing):
+            trail[i, :tr.shape[1]] = tr[0]
+        return embeds, mask, trail, pad_e
+
+    # -------------------------------------------------------------------------------- generate
+    @torch.no_grad()
+    def generate(self, input_ids=None, instruct_ids=None, ref_ids=None, voice_clone_prompt=None, languages=None,
+                 speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
+                 temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
+                 subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=0,
+                 use_graph=True, **kwargs):
+        """Same contract as Qwen3TTSForConditionalGeneration.generate (M:2022-2292):
+        returns (list of [F_i,16] int64 codes, list of [F_i,H] last hidden states)."""
+        emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
+                                                   voice_clone_prompt, ref_ids)
+        gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
+                       subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
+        return self.engine.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=use_graph)

@@ -1,0 +1,360 @@
+"""MI355X talker + code-predictor engine: prompt assembly, prefill, graph-captured per-frame decode.
+
+Replaces `Qwen3TTSForConditionalGeneration.generate` (M = qwen_tts/core/models/modeling_qwen3_tts.py,
+:2022-2292) including the nested transformers-4.57 GenerationMixin loops of the talker (:2272) and the
+code predictor (:1671-1680).  One frame = 15 code-predictor steps + one talker decode step + token
+choice, captured once into a HIP graph and replayed per 80 ms frame; every step-dependent quantity
+(positions, KV lengths, frame index) lives in device counters advanced by `qt_advance` inside the graph.
+Per-request state lives in a `Session` object, never on the module (fixes the reference's shared
+`rope_deltas` race).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _hip
+from . import kernels as K
+
+
+def _w(W, name, dev):
+    t = W[name]
+    if not isinstance(t, torch.Tensor):
+        t = torch.from_numpy(t)
+    return t.to(dev)
+
+
+class _Layer:
+    def __init__(self, W, pre, lc, wdt, dev):
+        g = lambda n: _w(W, f"{pre}.{n}", dev)  # noqa: E731
+        self.qkv = K.tile_linear(torch.cat([g("self_attn.q_proj.weight"), g("self_attn.k_proj.weight"),
+                                            g("self_attn.v_proj.weight")], 0), wdt)
+        self.o = K.tile_linear(g("self_attn.o_proj.weight"), wdt)
+        self.gu = K.tile_swiglu(g("mlp.gate_proj.weight"), g("mlp.up_proj.weight"), wdt)
+        self.down = K.tile_linear(g("mlp.down_proj.weight"), wdt)
+        self.in_ln = g("input_layernorm.weight").float().contiguous()
+        self.post_ln = g("post_attention_layernorm.weight").float().contiguous()
+        self.q_norm = g("self_attn.q_norm.weight").float().contiguous()
+        self.k_norm = g("self_attn.k_norm.weight").float().contiguous()
+
+
+class _Stack:
+    """One Qwen3 decoder stack (talker backbone or code predictor)."""
+
+    def __init__(self, W, prefix, lc, wdt, dev, npos):
+        self.H, self.I = lc["hidden_size"], lc["intermediate_size"]
+        self.Hq, self.Hkv, self.D = lc["num_attention_heads"], lc["num_key_value_heads"], lc["head_dim"]
+        self.eps = lc["rms_norm_eps"]
+        self.n_layers = lc["num_hidden_layers"]
+        self.layers = [_Layer(W, f"{prefix}.layers.{i}", lc, wdt, dev) for i in range(self.n_layers)]
+        self.norm = _w(W, f"{prefix}.norm.weight", dev).float().contiguous()
+        self.theta = lc["rope_theta"]
+        self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
+        self.qkv_w = (self.Hq + 2 * self.Hkv) * self.D
+
+    def ensure_rope(self, npos, dev):
+        if self.cos.shape[0] < npos:
+            self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
+
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys):
+        """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays."""
+        for li, L in enumerate(self.layers):
+            kc, vc = kv[0][li], kv[1][li]
+            K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, gamma=L.in_ln, eps=self.eps)
+            K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
+                       self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
+            K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
+                        meta["row_start"], meta["row_len"], scratch["att"], max_keys)
+            K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
+            K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, gamma=L.post_ln, eps=self.eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
+
+
+def _scratch(R, st: _Stack, dev):
+    f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+    return {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": f(R, st.Hq * st.D), "h": f(R, st.I)}
+
+
+@dataclass
+class GenParams:
+    max_new_tokens: int = 4096
+    do_sample: bool = True
+    top_k: int = 50
+    top_p: float = 1.0
+    temperature: float = 0.9
+    subtalker_dosample: bool = True
+    subtalker_top_k: int = 50
+    subtalker_top_p: float = 1.0
+    subtalker_temperature: float = 0.9
+    eos_token_id: Optional[int] = None
+    repetition_penalty: float = 1.05
+    ignore_eos: bool = False
+    seed: int = 0
+
+    def key(self):
+        return (self.do_sample, self.top_k, self.top_p, self.temperature, self.subtalker_dosample,
+                self.subtalker_top_k, self.subtalker_top_p, self.subtalker_temperature, self.eos_token_id,
+                self.repetition_penalty, self.ignore_eos, self.seed)
+
+
+class Session:
+    """Device buffers + captured frame graph for one (batch, capacity, params) shape."""
+
+    def __init__(self, eng: "TalkerEngine", B: int, P_cap: int, max_frames: int, gp: GenParams):
+        dev, t, c = eng.dev, eng.talker, eng.cp
+        self.B, self.P_cap, self.max_frames, self.gp = B, P_cap, max_frames, gp
+        self.Lmax = P_cap + max_frames + 2
+        i32 = lambda *s: torch.zeros(*s, dtype=torch.int32, device=dev)  # noqa: E731
+        kvd = eng.kv_dtype
+        self.kv = ([torch.zeros(B, t.Hkv, self.Lmax, t.D, dtype=kvd, device=dev) for _ in range(t.n_layers)],
+                   [torch.zeros(B, t.Hkv, self.Lmax, t.D, dtype=kvd, device=dev) for _ in range(t.n_layers)])
+        self.G = eng.G
+        self.cp_L = self.G + 1
+        self.cp_kv = ([torch.zeros(B, c.Hkv, self.cp_L, c.D, dtype=kvd, device=dev) for _ in range(c.n_layers)],
+                      [torch.zeros(B, c.Hkv, self.cp_L, c.D, dtype=kvd, device=dev) for _ in range(c.n_layers)])
+        # counters: [step, n_generated, rope_pos[B], kv_pos[B], kv_len[B]] advanced together each frame
+        self.ctr = i32(2 + 3 * B)
+        self.step, self.n_gen = self.ctr[0:1], self.ctr[1:2]
+        self.meta = {"rope_pos": self.ctr[2:2 + B], "kv_pos": self.ctr[2 + B:2 + 2 * B],
+                     "row_len": self.ctr[2 + 2 * B:2 + 3 * B], "row_start": i32(B),
+                     "row_batch": torch.arange(B, dtype=torch.int32, device=dev)}
+        # code predictor row metadata: prefill (2B rows) and per-step (B rows), static across frames
+        rb2 = torch.arange(2 * B, device=dev, dtype=torch.int32) // 2
+        p2 = torch.arange(2 * B, device=dev, dtype=torch.int32) % 2
+        self.cp_meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * B),
+                         "row_batch": rb2}
+        self.cp_meta = []
+        for g in range(1, self.G - 1):
+            pos = torch.full((B,), g + 1, dtype=torch.int32, device=dev)
+            self.cp_meta.append({"rope_pos": pos, "kv_pos": pos.clone(), "row_len": pos + 1, "row_start": i32(B),
+                                 "row_batch": self.meta["row_batch"]})
+        f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.x = f32(B, t.H)
+        self.past_hidden = f32(B, t.H)
+        self.logits = f32(B, eng.V)
+        self.cp_x = f32(2 * B, c.H)
+        self.cp_logits = f32(B, eng.Vc)
+        self.sc_t = _scratch(B, t, dev)
+        self.sc_c = _scratch(2 * B, c, dev)
+        self.codes = i32(B, max_frames + 2, self.G)
+        self.hiddens = f32(B, max_frames + 1, t.H)
+        self.tok0 = i32(B)
+        self.cp_tok = i32(B)
+        self.seen = torch.zeros(B, eng.V, dtype=torch.uint8, device=dev)
+        self.finished = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.trailing = f32(B, max_frames + 1, t.H)
+        self.pad_embed = f32(t.H)
+        self.graph = None
+
+
+class TalkerEngine:
+    def __init__(self, cfg: dict, weights: Dict[str, torch.Tensor], dtype: str = "bf16", device="cuda"):
+        _hip.lib()
+        self.cfg = cfg
+        self.tc = tc = cfg["talker_config"]
+        self.cc = cc = tc["code_predictor_config"]
+        self.dev = torch.device(device)
+        self.wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.kv_dtype = self.wdt
+        self.G = tc["num_code_groups"]
+        self.V, self.Vc = tc["vocab_size"], cc["vocab_size"]
+        W, dev, wdt = weights, self.dev, self.wdt
+        self.talker = _Stack(W, "talker.model", tc, wdt, dev, 4096)
+        self.cp = _Stack(W, "talker.code_predictor.model", cc, wdt, dev, self.G + 2)
+        self.codec_head = K.tile_linear(_w(W, "talker.codec_head.weight", dev), wdt)
+        self.emb0 = _w(W, "talker.model.codec_embedding.weight", dev).to(wdt).contiguous()
+        self.text_emb = _w(W, "talker.model.text_embedding.weight", dev).to(wdt).contiguous()
+        self.fc1 = K.tile_linear(_w(W, "talker.text_projection.linear_fc1.weight", dev), wdt,
+                                 _w(W, "talker.text_projection.linear_fc1.bias", dev))
+        self.fc2 = K.tile_linear(_w(W, "talker.text_projection.linear_fc2.weight", dev), wdt,
+                                 _w(W, "talker.text_projection.linear_fc2.bias", dev))
+        self.ecp = torch.stack([_w(W, f"talker.code_predictor.model.codec_embedding.{g}.weight", dev).to(wdt)
+                                for g in range(self.G - 1)]).contiguous()
+        self.lm_heads = [K.tile_linear(_w(W, f"talker.code_predictor.lm_head.{g}.weight", dev), wdt)
+                         for g in range(self.G - 1)]
+        s2m = "talker.code_predictor.small_to_mtp_projection.weight"
+        self.s2m = K.tile_linear(_w(W, s2m, dev), wdt, _w(W, s2m.replace("weight", "bias"), dev)) if s2m in W else None
+        self._sessions: Dict[tuple, Session] = {}
+        torch.cuda.synchronize()
+
+    # ---------------------------------------------------------------- G1: prompt embeddings
+    def text_proj(self, ids: torch.Tensor) -> torch.Tensor:
+        """text_projection(text_embedding(ids)) (M:808-816): gather -> fc1(+b, SiLU) -> fc2(+b); fp32 [n, H]."""
+        ids = ids.reshape(-1).to(self.dev, torch.int32)
+        n = ids.numel()
+        thd = self.text_emb.shape[1]
+        h = torch.empty(n, self.fc1.N, dtype=torch.float32, device=self.dev)
+        K.gemm(self.text_emb, self.fc1, h, n, thd, self.fc1.N, a_dtype=self.text_emb.dtype, a_index=ids,
+               act=_hip.ACT_SILU)
+        out = torch.empty(n, self.fc2.N, dtype=torch.float32, device=self.dev)
+        K.gemm(h, self.fc2, out, n, self.fc1.N, self.fc2.N)
+        return out
+
+    def codec_embed(self, ids) -> torch.Tensor:
+        ids = torch.as_tensor(ids, dtype=torch.int32, device=self.dev).reshape(-1)
+        H = self.talker.H
+        out = torch.empty(ids.numel(), H, dtype=torch.float32, device=self.dev)
+        K.gather_rows(self.emb0, ids, ids.numel(), H, out, H)
+        return out
+
+    def cp_embed(self, g, ids) -> torch.Tensor:
+        ids = torch.as_tensor(ids, dtype=torch.int32, device=self.dev).reshape(-1)
+        H = self.talker.H
+        out = torch.empty(ids.numel(), H, dtype=torch.float32, device=self.dev)
+        K.gather_rows(self.ecp[g], ids, ids.numel(), H, out, H)
+        return out
+
+    # ---------------------------------------------------------------- sessions / graph
+    def session(self, B, P, max_frames, gp: GenParams) -> Session:
+        P_cap = max(64, (P + 63) // 64 * 64)
+        key = (B, max_frames, gp.key())
+        s = self._sessions.get(key)
+        if s is None or s.P_cap < P:
+            s = Session(self, B, P_cap, max_frames, gp)
+            self.talker.ensure_rope(s.Lmax + 4, self.dev)
+            self._sessions = {key: s}  # keep one live session (HBM)
+        return s
+
+    def _eos(self, gp):
+        return gp.eos_token_id if gp.eos_token_id is not None else self.tc["codec_eos_token_id"]
+
+    def _sample_talker(self, s: Session, logits, codes_step_off, substep):
+        gp = s.gp
+        eos = self._eos(gp)
+        K.sample(logits, s.B, self.V, self.V, s.tok0, seen=s.seen, rep_penalty=gp.repetition_penalty,
+                 n_generated=s.n_gen, min_new_tokens=2, eos_id=eos,
+                 suppress=(self.V - 1024, self.V, self.tc["codec_eos_token_id"]), ignore_eos=gp.ignore_eos,
+                 finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
+                 temperature=gp.temperature, seed=gp.seed, step=s.step, substep=substep, codes=s.codes,
+                 codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off)
+
+    def _frame(self, s: Session):
+        """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
+        B, t, c, gp = s.B, self.talker, self.cp, s.gp
+        Hc = c.H
+        codes_ld = s.codes.shape[1] * self.G
+        # --- code predictor prefill: rows (2b, 2b+1) = (past_hidden[b], codec_embedding(tok0[b]))
+        if self.s2m is not None:
+            K.gemm(s.past_hidden, self.s2m, s.cp_x, B, t.H, 2 * Hc)
+            K.gemm(self.emb0, self.s2m, s.cp_x.view(-1)[Hc:], B, t.H, 2 * Hc,
+                   a_dtype=self.emb0.dtype, o_dtype=torch.float32, a_index=s.tok0)
+        else:
+            s.cp_x.view(B, 2, Hc)[:, 0].copy_(s.past_hidden)
+            K.gather_rows(self.emb0, s.tok0, B, Hc, s.cp_x.view(-1)[Hc:], 2 * Hc)
+        c.forward(s.cp_x, 2 * B, s.cp_meta0, s.cp_kv, s.sc_c, s.cp_L, s.cp_L)
+        self._cp_head(s, s.cp_x.view(-1)[Hc:], 2 * Hc, 0)
+        for g in range(1, self.G - 1):
+            x = s.cp_x[:B]
+            if self.s2m is not None:
+                K.gemm(self.ecp[g - 1], self.s2m, x, B, t.H, Hc, a_dtype=self.ecp.dtype, a_index=s.cp_tok)
+            else:
+                K.gather_rows(self.ecp[g - 1], s.cp_tok, B, Hc, x, Hc)
+            c.forward(x, B, s.cp_meta[g - 1], s.cp_kv, s.sc_c, s.cp_L, s.cp_L)
+            self._cp_head(s, x, Hc, g)
+        # --- talker decode input and forward
+        K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
+                      s.trailing.shape[1], s.pad_embed, s.x, B)
+        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax)
+        K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H)
+        K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
+        self._sample_talker(s, s.logits, 1, 0)
+        K.advance(s.ctr, 2 + 3 * B)
+
+    def _cp_head(self, s: Session, h, ldh, g):
+        c, gp = self.cp, s.gp
+        K.gemm(h, self.lm_heads[g], s.cp_logits, s.B, ldh, self.Vc, gamma=c.norm, eps=c.eps)
+        K.sample(s.cp_logits, s.B, self.Vc, self.Vc, s.cp_tok, do_sample=gp.subtalker_dosample,
+                 top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
+                 seed=gp.seed, step=s.step, substep=1 + g, codes=s.codes, codes_ld=s.codes.shape[1] * self.G,
+                 codes_w=self.G, codes_col=1 + g, codes_step_off=0)
+
+    # ---------------------------------------------------------------- G2/G3: prefill + decode loop
+    def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
+                             tts_pad: torch.Tensor, gp: GenParams, use_graph: bool = True, on_frames=None):
+        """embeds fp32 [B,P,H] left-padded, mask [B,P] -> (codes list [F_i,16] int64 cpu, hidden list)."""
+        B, P, H = embeds.shape
+        t = self.talker
+        max_frames = max(gp.max_new_tokens - 1, 0)
+        s = self.session(B, P, max(max_frames, 1), gp)
+        dev = self.dev
+        # reset per-request state
+        for z in (s.seen, s.finished, s.codes, s.ctr):
+            z.zero_()
+        # stale K/V beyond each row's valid range is never read (row_start/row_len bound every read)
+        Ttr = trailing.shape[1]
+        s.pad_embed.copy_(tts_pad.reshape(-1).float())
+        s.trailing.copy_(s.pad_embed.view(1, 1, H).expand_as(s.trailing))
+        n = min(Ttr, s.trailing.shape[1])
+        s.trailing[:, :n] = trailing[:, :n].to(dev).float()
+        # positions (get_rope_index + rope_deltas, M:1693-1711, 1746-1800)
+        mask = mask.to(dev)
+        pos = mask.float().cumsum(-1) - 1
+        pos = pos.masked_fill(mask == 0, 1)
+        max_pos = pos.max(-1)[0]
+        n_real = mask.sum(-1)
+        n_pads = P - n_real
+        rope_delta = (max_pos + 1 - n_real).long() - n_pads
+        R = B * P
+        pre_meta = {"rope_pos": pos.reshape(-1).to(torch.int32),
+                    "kv_pos": torch.arange(P, device=dev, dtype=torch.int32).repeat(B),
+                    "row_len": torch.arange(1, P + 1, device=dev, dtype=torch.int32).repeat(B),
+                    "row_start": torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])
+                    .reshape(-1).to(torch.int32),
+                    "row_batch": torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(P)}
+        x = embeds.to(dev).float().reshape(R, H).contiguous()
+        t.forward(x, R, pre_meta, s.kv, _scratch(R, t, dev), s.Lmax, P)
+        last = x.view(B, P, H)[:, -1].contiguous()
+        K.rmsnorm(last, t.norm, t.eps, s.past_hidden, B, H)
+        K.gemm(s.past_hidden, self.codec_head, s.logits, B, H, self.V)
+        self._sample_talker(s, s.logits, 0, 99)
+        # decode counters: step 0, one token generated, pos = P + delta, kv_pos = P, len = P + 1
+        s.ctr[1] = 1
+        s.meta["rope_pos"].copy_((P + rope_delta).to(torch.int32))
+        s.meta["kv_pos"].fill_(P)
+        s.meta["row_len"].fill_(P + 1)
+        s.meta["row_start"].copy_(n_pads.to(torch.int32))
+        frames = 0
+        if max_frames > 0:
+            if use_graph and s.graph is None:
+                s.graph = self._capture(s)
+            check_every = 8
+            while frames < max_frames:
+                s.hiddens[:, frames].copy_(s.past_hidden)
+                if use_graph:
+                    s.graph.replay()
+                else:
+                    self._frame(s)
+                frames += 1
+                if on_frames is not None:
+                    on_frames(s, frames)
+                if frames % check_every == 0 or frames == max_frames:
+                    if bool(s.finished.all()):
+                        break
+        codes = s.codes[:, :frames].long().cpu()
+        hid = s.hiddens[:, :frames].cpu()
+        eos = self.tc["codec_eos_token_id"]
+        out_c, out_h = [], []
+        for b in range(B):
+            c0 = codes[b, :, 0]
+            stop = (c0 == eos).nonzero()
+            L = int(stop[0]) if stop.numel() else frames
+            out_c.append(codes[b, :L])
+            out_h.append(hid[b, :L])
+        return out_c, out_h
+
+    def _capture(self, s: Session):
+        # the graph must not see the prefill-time counter values: it only reads device memory
+        snap = s.ctr.clone(), s.seen.clone(), s.finished.clone(), s.codes.clone(), s.tok0.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                self._frame(s)
+        torch.cuda.current_stream().wait_stream(side)
+        # capture does not execute kernels on ROCm/CUDA; restore anyway for safety
+        s.ctr.copy_(snap[0]); s.seen.copy_(snap[1]); s.finished.copy_(snap[2]); s.codes.copy_(snap[3])
+        s.tok0.copy_(snap[4])
+        return g

@@ -1,0 +1,54 @@
+"""Text processor stand-in for the Qwen2 BPE processor (qwen_tts/inference/qwen3_tts_model.py:278-285).
+
+A real `tokenizer.json` in the checkpoint dir is used through the `tokenizers` library when present.
+Offline there is none, so the fallback maps text deterministically to ids in
+[1000, 150000) while reproducing the special-token layout the reference slices on
+(`[:3]` role tokens, `[3:-5]` text, `[-5:]` suffix; M:2178-2231).
+"""
+from __future__ import annotations
+
+import os
+import re
+import zlib
+
+import torch
+
+SPECIAL = {"<|im_start|>": 151644, "<|im_end|>": 151645, "<tts_pad>": 151671, "<tts_text_bos>": 151672,
+           "<tts_text_eod>": 151673}
+WORDS = {"assistant": 77091, "user": 872, "\n": 198}
+_SPLIT = re.compile(r"(<\|im_start\|>|<\|im_end\|>|\n)")
+
+
+class FallbackProcessor:
+    def __call__(self, text, return_tensors="pt", padding=True):
+        ids = []
+        for part in _SPLIT.split(text):
+            if not part:
+                continue
+            if part in SPECIAL:
+                ids.append(SPECIAL[part])
+            elif part in WORDS:
+                ids.append(WORDS[part])
+            elif ids and ids[-1] == SPECIAL["<|im_start|>"] and part in WORDS:
+                ids.append(WORDS[part])
+            else:
+                for w in re.findall(r"\w+|[^\w\s]|\s+", part):
+                    if w in WORDS:
+                        ids.append(WORDS[w])
+                    else:
+                        ids.append(1000 + zlib.crc32(w.encode("utf-8")) % 149000)
+        return {"input_ids": torch.tensor([ids], dtype=torch.long)}
+
+
+def load_processor(path: str):
+    tj = os.path.join(path, "tokenizer.json")
+    if os.path.exists(tj):
+        from tokenizers import Tokenizer
+        tok = Tokenizer.from_file(tj)
+
+        class _P:
+            def __call__(self, text, return_tensors="pt", padding=True):
+                return {"input_ids": torch.tensor([tok.encode(text).ids], dtype=torch.long)}
+
+        return _P()
+    return FallbackProcessor()

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference golden vectors.
+
+Tolerances: codebook indices bit-exact (fp32 parity mode, greedy); PCM |diff| <= 2e-4 abs in fp32 mode,
+and in bf16 mode a relative L2 error <= 5e-2 (bf16 weights + activations vs the fp32 reference).
+Kernel unit tests compare against plain torch fp32 on the same seeded inputs.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+# ------------------------------------------------------------------------------------------ kernels
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (8, 256, 512), (16, 96, 160), (37, 128, 96), (130, 48, 64)])
+def test_gemm_linear(dtype, M, N, K):
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator(device="cpu").manual_seed(M * 1000 + N)
+    W = torch.randn(N, K, generator=g) * 0.1
+    A = torch.randn(M, K, generator=g)
+    b = torch.randn(N, generator=g) * 0.1
+    gamma = 1 + 0.1 * torch.randn(K, generator=g)
+    t = Kn.tile_linear(W.to(dev), dtype, b.to(dev))
+    out = torch.zeros(M, N, device=dev)
+    Kn.gemm(A.to(dev), t, out, M, K, N, gamma=gamma.to(dev), eps=1e-6)
+    Wr = W.to(dtype).float()
+    h = A * torch.rsqrt(A.pow(2).mean(-1, keepdim=True) + 1e-6) * gamma
+    if dtype == torch.bfloat16:
+        h = (A * gamma).to(dtype).float() * torch.rsqrt(A.pow(2).mean(-1, keepdim=True) + 1e-6)
+    ref = h @ Wr.T + b
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_swiglu_and_residual(dtype):
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(3)
+    M, H, I = 8, 128, 192
+    gate, up, down = (torch.randn(I, H, generator=g) * 0.05, torch.randn(I, H, generator=g) * 0.05,
+                      torch.randn(H, I, generator=g) * 0.05)
+    x = torch.randn(M, H, generator=g)
+    tgu, td = Kn.tile_swiglu(gate.to(dev), up.to(dev), dtype), Kn.tile_linear(down.to(dev), dtype)
+    h = torch.zeros(M, I, device=dev)
+    Kn.gemm(x.to(dev), tgu, h, M, H, I, epi=_hip.EPI_SWIGLU)
+    xr = x.to(dev).clone()
+    Kn.gemm(h, td, xr, M, I, H, epi=_hip.EPI_ADD)
+    c = lambda w: w.to(dtype).float()  # noqa: E731
+    xa = x.to(dtype).float() if dtype == torch.bfloat16 else x
+    hr = torch.nn.functional.silu(xa @ c(gate).T) * (xa @ c(up).T)
+    ha = hr.to(dtype).float() if dtype == torch.bfloat16 else hr
+    ref = x + ha @ c(down).T
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(h.cpu(), hr, atol=tol, rtol=tol)
+    torch.testing.assert_close(xr.cpu(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("cin,cout,k,dil", [(32, 48, 3, 1), (64, 16, 7, 3), (24, 40, 1, 1), (96, 1, 7, 1)])
+def test_gemm_causal_conv(cin, cout, k, dil):
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(cin + cout)
+    B, T = 2, 37
+    w, b = torch.randn(cout, cin, k, generator=g) * 0.1, torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(B, cin, T, generator=g)
+    ref = torch.nn.functional.conv1d(torch.nn.functional.pad(x, ((k - 1) * dil, 0)), w, b, dilation=dil)
+    t = Kn.tile_conv(w.to(dev), b.to(dev), torch.float32, dil)
+    xl = x.permute(0, 2, 1).contiguous().to(dev)
+    out = torch.zeros(B * T, cout, device=dev)
+    Kn.gemm(xl, t, out, B * T, cin, cout, conv=(T, T, -(k - 1) * dil, dil))
+    torch.testing.assert_close(out.view(B, T, cout).permute(0, 2, 1).cpu(), ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("cin,cout,s", [(32, 16, 2), (64, 32, 5), (16, 8, 3)])
+def test_gemm_transposed_conv(cin, cout, s):
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(s)
+    B, T = 2, 11
+    x = torch.randn(B, cin, T, generator=g)
+    for k in (s, 2 * s):
+        w, b = torch.randn(cin, cout, k, generator=g) * 0.1, torch.randn(cout, generator=g) * 0.1
+        y = torch.nn.functional.conv_transpose1d(x, w, b, stride=s)
+        pad = k - s
+        ref = y[..., pad:y.shape[-1] - pad]
+        t = Kn.tile_transconv(w.to(dev), b.to(dev), torch.float32, s)
+        tout = T if k == s else T - 1
+        out = torch.zeros(B * tout * s, cout, device=dev)
+        Kn.gemm(x.permute(0, 2, 1).contiguous().to(dev), t, out, B * tout, cin, s * cout, conv=(T, tout, 0, 1))
+        torch.testing.assert_close(out.view(B, tout * s, cout).permute(0, 2, 1).cpu(), ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("D,hq,hkv,window", [(128, 16, 8, 0), (16, 4, 2, 0), (64, 4, 4, 5)])
+def test_qkv_post_and_attention(D, hq, hkv, window):
+    from qwen_tts import kernels as Kn
+    from oracle.talker import apply_rope, rmsnorm, rope_cos_sin
+    dev = _dev()
+    g = torch.Generator().manual_seed(D + hq)
+    B, L = 3, 23
+    qkv = torch.randn(B * L, (hq + 2 * hkv) * D, generator=g)
+    qn, kn = 1 + 0.1 * torch.randn(D, generator=g), 1 + 0.1 * torch.randn(D, generator=g)
+    pos = torch.arange(L).repeat(B)
+    starts = torch.tensor([0, 4, 9])
+    cos, sin = Kn.rope_tables(D, 1e6, 64, dev)
+    rb = torch.arange(B).repeat_interleave(L)
+    kc = torch.zeros(B, hkv, L, D, device=dev)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(B * L, hq * D, device=dev)
+    i32 = lambda t: t.to(dev, torch.int32)  # noqa: E731
+    use_norm = window == 0
+    Kn.qkv_post(qkv.to(dev), B * L, hq, hkv, D, qn.to(dev) if use_norm else None, kn.to(dev) if use_norm else None,
+                1e-6, cos, sin, i32(pos), i32(rb), i32(pos), q, kc, vc, L)
+    row_start = starts.repeat_interleave(L)
+    row_len = torch.maximum(pos + 1, row_start + 1)
+    att = torch.zeros(B * L, hq * D, device=dev)
+    Kn.attention(q, B * L, hq, hkv, D, kc, vc, L, i32(rb), i32(row_start), i32(row_len), att, L, window=window)
+    # torch reference
+    x = qkv.view(B, L, hq + 2 * hkv, D)
+    qr, kr, vr = x[:, :, :hq], x[:, :, hq:hq + hkv], x[:, :, hq + hkv:]
+    if use_norm:
+        qr, kr = rmsnorm(qr, qn, 1e-6), rmsnorm(kr, kn, 1e-6)
+    c, s = rope_cos_sin(torch.arange(L)[None].expand(B, L), D, 1e6)
+    qr, kr = apply_rope(qr.transpose(1, 2), c, s), apply_rope(kr.transpose(1, 2), c, s)
+    torch.testing.assert_close(kc.cpu(), kr, atol=1e-5, rtol=1e-5)
+    kr, vr = kr.repeat_interleave(hq // hkv, 1), vr.transpose(1, 2).repeat_interleave(hq // hkv, 1)
+    sc = qr @ kr.transpose(2, 3) * D ** -0.5
+    kv = torch.arange(L)
+    allowed = kv[None, :] <= torch.arange(L)[:, None]
+    allowed = allowed[None] & (kv[None, None, :] >= starts[:, None, None])
+    if window:
+        allowed = allowed & (kv[None, None, :] > torch.arange(L)[None, :, None] - window)
+    allowed = allowed | (kv[None, None, :] == torch.maximum(torch.arange(L)[None, :, None], starts[:, None, None]))
+    sc = sc.masked_fill(~allowed[:, None], float("-inf"))
+    ref = (sc.softmax(-1) @ vr).transpose(1, 2).reshape(B * L, hq * D)
+    torch.testing.assert_close(att.cpu(), ref, atol=2e-5, rtol=2e-5)
+
+
+def test_sample_greedy_processors():
+    from qwen_tts import kernels as Kn
+    from oracle.talker import process_logits
+    dev = _dev()
+    g = torch.Generator().manual_seed(5)
+    B, V, eos = 4, 3072, 2150
+    logits = torch.randn(B, V, generator=g)
+    logits[0, 2150] = 50.0  # eos wins if not masked
+    logits[1, 7] = logits[1, 9] = 40.0  # tie -> lowest index
+    hist = torch.randint(0, 2048, (B, 5), generator=g)
+    hist[2, 0] = int(torch.argmax(logits[2, :2048]))  # penalised winner
+    seen = torch.zeros(B, V, dtype=torch.uint8)
+    seen.scatter_(1, hist, 1)
+    supp = [i for i in range(V - 1024, V) if i != eos]
+    for ngen in (1, 5):
+        ref = torch.argmax(process_logits(logits, hist, ngen, eos, supp, 1.05), -1)
+        tok = torch.zeros(B, dtype=torch.int32, device=dev)
+        sd = seen.to(dev)
+        Kn.sample(logits.to(dev), B, V, V, tok, seen=sd, rep_penalty=1.05,
+                  n_generated=torch.tensor([ngen], dtype=torch.int32, device=dev), min_new_tokens=2, eos_id=eos,
+                  suppress=(V - 1024, V, eos))
+        assert tok.cpu().long().tolist() == ref.tolist()
+
+
+def test_sample_distribution_topk():
+    """Sampling parity is distribution-level (RNG streams differ by device): frequencies vs probabilities."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    V, R = 64, 2048
+    logits = torch.linspace(-2, 2, V)[None].expand(R, V).contiguous()
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=8, top_p=1.0, temperature=0.9, seed=11,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    t = tok.cpu().long()
+    assert t.min() >= V - 8
+    p = torch.softmax(logits[0, V - 8:] / 0.9, -1)
+    freq = torch.bincount(t - (V - 8), minlength=8).float() / R
+    assert (freq - p).abs().max() < 0.05
+
+
+# ------------------------------------------------------------------------------------------ end-to-end talker
+@pytest.fixture(scope="module")
+def tiny_models():
+    from oracle import load_preset, synth_state_dict, talker_param_specs
+    from qwen_tts.model import TTSModel
+    _dev()
+    out = {}
+    for p in ("tiny-customvoice", "tiny-voicedesign"):
+        cfg, _ = load_preset(p)
+        W = {k: torch.from_numpy(v) for k, v in synth_state_dict(talker_param_specs(cfg)).items()}
+        out[p] = (cfg, W, TTSModel(cfg, W, dtype="fp32"))
+    return out
+
+
+def _run_case(model, key, case, idx, cfg, use_graph=True):
+    from cases import gen_kwargs, make_inputs
+    ids, ins, vcp, ref_ids = make_inputs(case, idx, cfg["talker_config"]["hidden_size"])
+    return model.generate(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp,
+                          languages=case["languages"], speakers=case["speakers"],
+                          non_streaming_mode=case["non_streaming_mode"], use_graph=use_graph, **gen_kwargs(case))
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_talker_greedy_codes_bit_exact(tiny_models, use_graph):
+    from cases import talker_cases
+    z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+    cases = talker_cases()
+    for idx, (key, case) in enumerate(cases.items()):
+        if case.get("do_sample"):
+            continue
+        preset = "tiny-voicedesign" if key.startswith("vd_") else "tiny-customvoice"
+        cfg, _, model = tiny_models[preset]
+        codes, hid = _run_case(model, key, case, idx, cfg, use_graph)
+        assert len(codes) == int(z[f"{key}/n"]), key
+        for j, c in enumerate(codes):
+            np.testing.assert_array_equal(c.numpy(), z[f"{key}/codes{j}"], err_msg=key)
+            np.testing.assert_allclose(hid[j].numpy(), z[f"{key}/hidden{j}"], atol=2e-4, rtol=2e-4, err_msg=key)
+
+
+def test_talker_eos_ragged_bit_exact(tiny_models):
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    W = dict(W)
+    head = W["talker.codec_head.weight"].clone()
+    head[cfg["talker_config"]["codec_eos_token_id"]] = head[int(z["eos_b2/donor"])]
+    W["talker.codec_head.weight"] = head
+    model = TTSModel(cfg, W, dtype="fp32")
+    cases = talker_cases()
+    key = "cv_b2_stream_dialect"
+    codes, _ = _run_case(model, key, dict(cases[key], max_new_tokens=24), list(cases).index(key), cfg)
+    for j, c in enumerate(codes):
+        np.testing.assert_array_equal(c.numpy(), z[f"eos_b2/codes{j}"])
+
+
+def test_talker_bf16_runs_and_tracks_fp32(tiny_models):
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, m32 = tiny_models["tiny-customvoice"]
+    m16 = TTSModel(cfg, W, dtype="bf16")
+    case = talker_cases()["cv_b1_nonstream"]
+    c32, _ = _run_case(m32, "cv_b1_nonstream", case, 0, cfg)
+    c16, _ = _run_case(m16, "cv_b1_nonstream", case, 0, cfg)
+    assert c16[0].shape == c32[0].shape
+    assert (c16[0][:2, 0] == c32[0][:2, 0]).all()  # the first tokens agree; later frames may drift in bf16
+
+
+# ------------------------------------------------------------------------------------------ codec
+@pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice")])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_codec_decode_matches_reference(fname, preset, dtype):
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    _dev()
+    z = np.load(os.path.join(GOLD, fname))
+    _, ccfg = load_preset(preset)
+    W = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    tok = Qwen3TTSTokenizer.from_pretrained(f"synthetic:{preset}/speech_tokenizer", dtype=dtype, weights=W)
+    for key in sorted({k.split("/")[0] for k in z.files}):
+        n = len([k for k in z.files if k.startswith(key + "/codes")])
+        codes = [z[f"{key}/codes{j}"].astype(np.int64) for j in range(n)]
+        wavs, sr = tok.decode([{"audio_codes": c} for c in codes])
+        assert sr == 24000
+        for j, w in enumerate(wavs):
+            assert w.shape[0] == int(z[f"{key}/len{j}"]), key
+            ref = z[f"{key}/wav{j}"] if f"{key}/wav{j}" in z.files else None
+            got = w if ref is not None else w[::7]
+            ref = ref if ref is not None else z[f"{key}/wav{j}_stride"]
+            if dtype == "fp32":
+                np.testing.assert_allclose(got, ref, atol=2e-4, rtol=0, err_msg=key)
+            else:
+                rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+                assert rel < 5e-2, (key, rel)
