@@ -1,0 +1,240 @@
+"""Benchmark: Qwen3-TTS-12Hz-1.7B CustomVoice, batch 8 x 200-token prompts, streaming-text decode
+(BASELINE.json configs[2]) on the MI355X HIP path.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = prefill + 256 AR frames (talker + 15-step code predictor per frame, HIP-graph replay) +
+12 Hz codec decode of all 8 utterances to 24 kHz PCM.  Weak scaling: every rank serves its own batch of
+8 independent utterances (data parallel, no collective on the data path; RCCL only broadcasts the
+weights at init).  Weights are seeded synthetic at the ASSUMED 1.7B dims (no checkpoint offline).
+value = sum over ranks of generated audio seconds / max-over-ranks wall time of the K timed steps.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts_amd"))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def synth_ids(n, seed):
+    g = np.random.default_rng([1234, seed])
+    body = g.integers(1000, 150000, n).tolist()
+    return torch.tensor([[151644, 77091, 198] + body + [151645, 198, 151644, 77091, 198]], dtype=torch.long)
+
+
+def make_weights(preset, dev, world, rank):
+    import torch.distributed as dist
+    from qwen_tts.weights import codec_specs, read_json, resolve_path, synthetic, talker_specs
+    d = resolve_path(f"synthetic:{preset}")
+    cfg = read_json(os.path.join(d, "config.json"))
+    ccfg = read_json(os.path.join(d, "speech_tokenizer", "config.json"))
+    specs_t, specs_c = talker_specs(cfg), codec_specs(ccfg)
+    if world > 1:  # rank 0 generates, RCCL broadcast over xGMI (the only collective of the design)
+        W = synthetic(specs_t, dev) if rank == 0 else {n: torch.empty(s, device=dev) for n, s in specs_t}
+        CW = synthetic(specs_c, dev) if rank == 0 else {n: torch.empty(s, device=dev) for n, s in specs_c}
+        for t in list(W.values()) + list(CW.values()):
+            dist.broadcast(t, 0)
+    else:
+        W, CW = synthetic(specs_t, dev), synthetic(specs_c, dev)
+    return cfg, W, CW
+
+
+class GemmRecorder:
+    """Times every qt_gemm launch of one eager frame with HIP events (same stream) and sums the
+    algorithmic bytes each launch must move: weights + activations in + activations out."""
+
+    def __init__(self):
+        self.recs = []
+
+    def __call__(self, fn, A, W, out, M, *a, **k):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        fn(A, W, out, M, *a, **k)
+        ev1.record()
+        wbytes = W.w.numel() * W.w.element_size()
+        abytes = M * W.K * (A.element_size() if k.get("a_dtype") is None else 2)
+        obytes = M * W.N * out.element_size() * (2 if k.get("epi") == 1 else 1)
+        self.recs.append((ev0, ev1, wbytes + abytes + obytes, M))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b, _, _ in self.recs]
+        by = [r[2] for r in self.recs]
+        n = len(ms)
+        tot_ms, tot_b = sum(ms), sum(by)
+        return dict(launches=n, avg_us=1e3 * tot_ms / n, bytes_per_launch=tot_b / n, gbs=tot_b / (tot_ms * 1e-3) / 1e9)
+
+
+def kernel_roofline(tts, ids, languages, speakers, frames):
+    """One extra eager (non-graph) generate of a few frames with per-launch HIP events on qt_gemm."""
+    from qwen_tts import kernels as Kn
+    rec = GemmRecorder()
+    orig = Kn.gemm
+    started = {"on": False}
+
+    def hooked(A, W, out, M, *a, **k):
+        if started["on"]:
+            rec(orig, A, W, out, M, *a, **k)
+        else:
+            orig(A, W, out, M, *a, **k)
+
+    eng = tts.model.engine
+
+    def on_frames(s, n):
+        started["on"] = n >= 1  # skip the prefill; record the decode frames
+
+    Kn.gemm = hooked
+    try:
+        from qwen_tts.talker import GenParams
+        emb, mask, trail, pad = tts.model.build_prompts(ids, languages, speakers, None, False)
+        gp = GenParams(max_new_tokens=frames + 1, ignore_eos=True)
+        eng.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=False, on_frames=on_frames)
+    finally:
+        Kn.gemm = orig
+    return rec.summary()
+
+
+def cpu_baseline(B, prompt, frames, threads):
+    """Oracle (CPU fp32 restatement of the reference) on a bounded sample of the same workload."""
+    from oracle import CodecOracle, TalkerOracle, build_prompts, codec_param_specs, generate, load_preset
+    from oracle.talker import talker_param_specs
+    torch.set_num_threads(threads)
+    cfg, ccfg = load_preset("1.7b-customvoice")
+    g = torch.Generator().manual_seed(0)
+    W = {n: 0.02 * torch.randn(s, generator=g) for n, s in talker_param_specs(cfg)}
+    CW = {n: 0.02 * torch.randn(s, generator=g) for n, s in codec_param_specs(ccfg)}
+    o, co = TalkerOracle(cfg, W), CodecOracle(ccfg, CW)
+    ids = [synth_ids(prompt, i) for i in range(B)]
+    spk = ["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"][:B]
+    t0 = time.time()
+    with torch.no_grad():
+        emb, mask, trail, pad = build_prompts(o, ids, ["english"] * B, (spk * 8)[:B], None, False)
+        res = generate(o, emb, mask, trail, pad, max_new_tokens=frames + 1, do_sample=True, ignore_eos=True)
+        codes = torch.stack(res.codes)
+        wav = co.decode(codes)
+    dt = time.time() - t0
+    audio = sum(w.shape[0] for w in wav) / 24000.0
+    return dict(value=audio / dt, unit="audio-seconds/sec", cores=threads, kind="port",
+                sample=f"oracle fp32, 1.7B dims, B={B} x {prompt}-token prompts, {frames} frames + codec, {dt:.1f}s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--prompt-tokens", type=int, default=200)
+    ap.add_argument("--preset", default="1.7b-customvoice")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--roofline", type=int, default=1)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from qwen_tts import Qwen3TTSModel
+    cfg, W, CW = make_weights(a.preset, dev, world, rank)
+    tts = Qwen3TTSModel.from_pretrained(f"synthetic:{a.preset}", device_map=str(dev),
+                                        dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32,
+                                        weights=W, codec_weights=CW)
+    del W, CW
+    torch.cuda.empty_cache()
+    B = a.batch
+    ids = [synth_ids(a.prompt_tokens, rank * 1000 + i) for i in range(B)]
+    spk = (["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"] * 8)[:B]
+    langs = ["english"] * B
+    gen = dict(max_new_tokens=a.frames + 1, do_sample=True, top_k=50, top_p=1.0, temperature=0.9,
+               subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9,
+               repetition_penalty=1.05, ignore_eos=True)
+
+    def step(seed):
+        t0 = time.perf_counter()
+        codes, _ = tts.model.generate(input_ids=ids, languages=langs, speakers=spk, non_streaming_mode=False,
+                                      seed=seed, **gen)
+        wavs, sr = tts.model.speech_tokenizer.decode([{"audio_codes": c} for c in codes])
+        return sum(w.shape[0] for w in wavs) / sr, time.perf_counter() - t0
+
+    for i in range(a.warmup):
+        step(100 + i)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    audio, lat = 0.0, []
+    for i in range(a.steps):
+        s_audio, s_t = step(i)
+        audio += s_audio
+        lat.append(s_t)
+    barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt, audio], dtype=torch.float64, device=dev)
+    if dist is not None:
+        mx = tt[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt[1:].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        dt, audio = float(mx), float(sm)
+    value = audio / dt
+    roof = None
+    if a.roofline and rank == 0:
+        r = kernel_roofline(tts, ids, langs, spk, 4)
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_gemm_decode.json")
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": "gemm_wt<bf16,f32,f32,1,8> (decode weight-streaming GEMV)",
+                "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes_per_launch"]),
+                "launches_per_frame": r["launches"] // 3}
+    cpu = None
+    if a.cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    if rank == 0:
+        per_utt_rtf = value / (B * world)
+        out = {"metric": "audio-seconds/sec (RTF) + p50 first-packet latency, 1.7B @ batch 1/8, 1->8 GPU",
+               "value": round(value, 3), "unit": "audio-seconds/sec", "n_gpus": world, "steps": a.steps,
+               "warmup": a.warmup, "ms_per_step": round(1e3 * dt / a.steps, 2), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (seeded weights + token ids)",
+               "config": {"workload": f"Qwen3-TTS-12Hz-{a.preset} B={B}/GPU x {a.prompt_tokens}-token prompts, "
+                                      f"streaming text, {a.frames} frames + codec decode",
+                          "global_batch": B * world, "seq_len": a.prompt_tokens, "frames": a.frames,
+                          "parallelism": f"dp{world}"},
+               "rtf_per_utterance": round(per_utt_rtf, 2),
+               "first_packet_p50_ms": round(1e3 * float(np.median(lat)), 1),
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

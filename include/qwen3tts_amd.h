@@ -32,7 +32,8 @@ enum { QT_OK = 0, QT_ERR_ARG = -1, QT_ERR_SHAPE = -2, QT_ERR_DTYPE = -3, QT_ERR_
  *   talker & code predictor q/k/v/o, gate/up/down, codec_head, lm_head[g], small_to_mtp_projection,
  *   text_projection (M:740-751, 848-850, 1167-1174, 1575-1579);  codec pre_conv, transformer linears,
  *   ConvNeXt pwconv, decoder convs / transposed convs (K:159-242, 294-369, 492-493, 618-657, 838-864).
- * Fused prologues: RMSNorm (gamma != NULL; Qwen3TTSRMSNorm M:595-610 feeding the Linear), row gather
+ * Fused prologues: RMSNorm (rmsnorm != 0 or gamma != NULL: out *= rsqrt(mean_k A^2 + eps) per row;
+ * gamma scales A, or is folded into W at load time -- Qwen3TTSRMSNorm M:595-610 feeding the Linear), row gather
  * (a_index != NULL; nn.Embedding feeding the Linear), implicit im2col (taps > 0).
  * Fused epilogues: bias, SiLU / GELU, colscale (LayerScale K:393-405, ConvNeXt gamma K:236),
  * residual add (QT_EPI_ADD, M:1409/1417), SwiGLU (QT_EPI_SWIGLU; W rows interleaved 8 gate / 8 up per
@@ -51,6 +52,7 @@ typedef struct qt_gemm_args {
   const void* W;
   const float* gamma;
   float eps;
+  int rmsnorm;
   const float* bias;
   const float* colscale;
   int act;

@@ -21,7 +21,7 @@ struct GemmP {
   const void* A; long long lda;
   const int* a_index;
   const void* W;
-  const float* gamma; float eps;
+  const float* gamma; float eps; int rms;
   const float* bias; const float* colscale;
   int act, epi;
   void* out; long long ldo;
@@ -67,7 +67,8 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
   const int ktiles = p.Kp / KT;
   const int per = (ktiles + WPB - 1) / WPB;
   const int kt0 = w * per, kt1 = min(ktiles, kt0 + per);
-  const bool norm = p.gamma != nullptr;
+  const bool norm = p.rms != 0;
+  const bool hasg = p.gamma != nullptr;
 
   f32x4_t acc[MT];
   float ss[MT];
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
     u32x4_t wv = *(const u32x4_t*)(wp + (size_t)kt * 64 * E);
     const int kk = kt * KT + lk * E;
     float g[E];
-    if (norm) {
+    if (hasg) {
 #pragma unroll
       for (int i = 0; i < E; ++i) g[i] = (kk + i < p.Klog) ? p.gamma[kk + i] : 0.f;
     }
@@ -89,7 +90,11 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
       load_a<AT, E>(p, m0 + mt * 16 + lm, kk, a);
       if (norm) {
 #pragma unroll
-        for (int i = 0; i < E; ++i) { ss[mt] += a[i] * a[i]; a[i] *= g[i]; }
+        for (int i = 0; i < E; ++i) ss[mt] += a[i] * a[i];
+      }
+      if (hasg) {
+#pragma unroll
+        for (int i = 0; i < E; ++i) a[i] *= g[i];
       }
       if constexpr (BF) {
         u32x4_t av = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(a[4], a[5]), pack2bf(a[6], a[7])};
@@ -164,11 +169,129 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
   }
 }
 
+// Decode GEMV (M <= 16, plain or gathered rows, K % KT == 0): one wave owns a 16-row n-tile over a K
+// slice.  Branch-free inner loop: the lane's A row pointer is hoisted, tail tiles are clamped and zeroed
+// by select, so every chunk issues its U weight fragments (1 KiB contiguous per wave-instruction), A
+// fragments and gamma before a single wait -- the block keeps all of its weight bytes in flight.
+// Split-K partials reduce through LDS; the epilogue is shared with gemm_wt.
+template <typename WT, typename AT, typename OT, int WPB, int U, bool NORM>
+__global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
+  constexpr bool BF = sizeof(WT) == 2;
+  constexpr int E = BF ? 8 : 4;
+  constexpr int KT = 4 * E;
+  __shared__ float red[WPB][64][4];
+  __shared__ float red_ss[WPB][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lm = lane & 15, lk = lane >> 4;
+  const int nt = blockIdx.x;
+  const int ktiles = p.Kp / KT;
+  const int per = (ktiles + WPB - 1) / WPB;
+  const int kt0 = w * per, kt1 = min(ktiles, kt0 + per);
+  const bool rowok = lm < p.M;
+  const int mrow = rowok ? lm : p.M - 1;
+  const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[mrow] : (long long)mrow) * p.lda + lk * E;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  const WT* wp = (const WT*)p.W + ((size_t)nt * ktiles) * 64 * E + lane * E;
+  for (int c = kt0; c < kt1; c += U) {
+    u32x4_t wv[U];
+    float a[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kc = min(c + u, kt1 - 1);
+      wv[u] = *(const u32x4_t*)(wp + (size_t)kc * 64 * E);
+      if constexpr (E == 8) load8f(arow + kc * KT, a[u]); else load4f(arow + kc * KT, a[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = rowok && (c + u < kt1);
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        float x = ok ? a[u][i] : 0.f;
+        if constexpr (NORM) ss += x * x;
+        a[u][i] = x;
+      }
+      if constexpr (BF) {
+        u32x4_t av = {pack2bf(a[u][0], a[u][1]), pack2bf(a[u][2], a[u][3]), pack2bf(a[u][4], a[u][5]),
+                      pack2bf(a[u][6], a[u][7])};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
+                                                      __builtin_bit_cast(bf16x8_t, wv[u]), acc, 0, 0, 0);
+      } else {
+        f32x4_t wf = __builtin_bit_cast(f32x4_t, wv[u]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][s], wf[s], acc, 0, 0, 0);
+      }
+    }
+  }
+  red[w][lane][0] = acc[0]; red[w][lane][1] = acc[1]; red[w][lane][2] = acc[2]; red[w][lane][3] = acc[3];
+  if (NORM) {
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lk == 0) red_ss[w][lm] = ss;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ww = 0; ww < WPB; ++ww) {
+    v[0] += red[ww][lane][0]; v[1] += red[ww][lane][1]; v[2] += red[ww][lane][2]; v[3] += red[ww][lane][3];
+  }
+  const int n = nt * 16 + lm;
+  const bool nval = n < p.N;
+  const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
+  const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float x = v[i];
+    if (NORM) {
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WPB; ++ww) s += red_ss[ww][lk * 4 + i];
+      x *= rsqrtf(s / (float)p.Klog + p.eps);
+    }
+    x += bias;
+    if (p.act == QT_ACT_SILU) x = silu_f(x);
+    else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+    v[i] = x * cs;
+  }
+  OT* out = (OT*)p.out;
+  if (p.epi == QT_EPI_SWIGLU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float up = __shfl_xor(v[i], 8, 64);
+      const int m = lk * 4 + i;
+      if (lm < 8 && m < p.M && nt * 8 + lm < (p.N >> 1))
+        out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[i]) * up);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = lk * 4 + i;
+    if (m >= p.M || !nval) continue;
+    OT* o = out + (long long)m * p.ldo + n;
+    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[i]);
+    else *o = from_f<OT>(v[i]);
+  }
+}
+
+template <typename WT, typename AT, typename OT, int WPB>
+void launch_gemv(const GemmP& p, int nt, hipStream_t s) {
+  if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, 4, true>), dim3(nt), dim3(WPB * 64), 0, s, p);
+  else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, 4, false>), dim3(nt), dim3(WPB * 64), 0, s, p);
+}
+
 template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
-  if (p.M <= 16) {
-    hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, (p.M + 15) / 16), dim3(512), 0, s, p);
+  constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
+  if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr) {
+    const int kts = p.Kp / KT;
+    if (kts >= 48) launch_gemv<WT, AT, OT, 16>(p, nt, s);
+    else if (kts >= 16) launch_gemv<WT, AT, OT, 8>(p, nt, s);
+    else launch_gemv<WT, AT, OT, 4>(p, nt, s);
+  } else if (p.M <= 16) {
+    hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
   } else if (p.M <= 32) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 2, 8>), dim3(nt, (p.M + 31) / 32), dim3(512), 0, s, p);
   } else {
@@ -212,7 +335,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   if (a->M <= 0 || a->N <= 0 || (a->epi == QT_EPI_SWIGLU && a->N % 16)) return QT_ERR_SHAPE;
   if (a->epi == QT_EPI_SWIGLU && (a->bias || a->colscale)) return QT_ERR_ARG;
   p.A = a->A; p.lda = a->lda; p.a_index = a->a_index; p.W = a->W;
-  p.gamma = a->gamma; p.eps = a->eps; p.bias = a->bias; p.colscale = a->colscale;
+  p.gamma = a->gamma; p.eps = a->eps; p.rms = a->rmsnorm || a->gamma != nullptr; p.bias = a->bias; p.colscale = a->colscale;
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
   hipStream_t s = (hipStream_t)stream;
   const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;

@@ -1,12 +1,18 @@
 // Logits processing + token selection (transformers 4.57 semantics), one 256-thread block per row.
-// Greedy: argmax with lowest-index tie break (torch.argmax).  Sampling: Temperature -> TopK -> TopP
-// -> softmax -> inverse-CDF draw from a Philox-4x32-10 stream keyed by (seed, step, substep, row);
-// distribution-level parity with torch.multinomial (RNG streams differ by device).
+// Each thread keeps its V/256 (<= 16) scores in registers (strided, coalesced loads).
+// Greedy: argmax with lowest-index tie break (torch.argmax).
+// Sampling: Temperature -> TopK -> TopP -> softmax -> draw from a Philox-4x32-10 stream keyed by
+// (seed, step, substep, row).  Top-k threshold = exact k-th largest score, found by building its
+// order-preserving 32-bit key MSB-first (32 block-wide counts, no sort); ties at the threshold are kept
+// like TopKLogitsWarper.  The draw is an inverse CDF over a fixed category order (parallel prefix of
+// per-thread masses), so it is an exact sample of the warped distribution; RNG streams differ from
+// torch.multinomial, hence parity is distribution-level (tests/test_gpu_parity.py).
 #include "common.h"
 
 namespace {
 
-constexpr int MAXV = 4096;
+constexpr int NT = 256;
+constexpr int PER = 16;  // V <= 4096
 
 QT_DEV unsigned mulhilo(unsigned a, unsigned b, unsigned* hi) {
   unsigned long long p = (unsigned long long)a * b;
@@ -29,31 +35,56 @@ QT_DEV float philox_uniform(unsigned long long seed, unsigned c0, unsigned c1, u
   return ((x0 >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
 }
 
-__global__ __launch_bounds__(256) void sample_k(qt_sample_args p) {
-  __shared__ float sc[MAXV];
-  __shared__ float srt[MAXV];
-  __shared__ float rv[4];
-  __shared__ int ri[4];
+QT_DEV unsigned okey(float f) {  // order-preserving float -> uint
+  unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+QT_DEV float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+QT_DEV float block_max(float v, float* sh) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+}
+
+__global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
+  __shared__ float sh[8];
+  __shared__ int shi[4];
+  __shared__ float srt[4096];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = p.V;
   const float* lg = p.logits + (long long)r * p.ld;
   const bool fin = p.finished && p.finished[r];
   const int ngen = p.n_generated ? *p.n_generated : 1 << 30;
-  for (int v = tid; v < V; v += 256) {
-    float s = lg[v];
-    if (p.seen && p.rep_penalty != 1.0f && p.seen[(long long)r * V + v]) s = s < 0.f ? s * p.rep_penalty : s / p.rep_penalty;
-    if (p.eos_id >= 0 && v == p.eos_id && (ngen < p.min_new_tokens || p.ignore_eos)) s = -INFINITY;
-    if (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) s = -INFINITY;
-    sc[v] = s;
+  float s[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int v = tid + j * NT;
+    float x = -INFINITY;
+    if (v < V) {
+      x = lg[v];
+      if (p.seen && p.rep_penalty != 1.0f && p.seen[(long long)r * V + v]) x = x < 0.f ? x * p.rep_penalty : x / p.rep_penalty;
+      if (p.eos_id >= 0 && v == p.eos_id && (ngen < p.min_new_tokens || p.ignore_eos)) x = -INFINITY;
+      if (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) x = -INFINITY;
+    }
+    s[j] = x;
   }
-  __syncthreads();
   int tok;
   if (!p.do_sample) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int v = tid; v < V; v += 256) {
-      float s = sc[v];
-      if (s > best || (s == best && v < bi)) { best = s; bi = v; }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int v = tid + j * NT;
+      if (v < V && (s[j] > best || (s[j] == best && v < bi))) { best = s[j]; bi = v; }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -61,88 +92,104 @@ __global__ __launch_bounds__(256) void sample_k(qt_sample_args p) {
       int oi = __shfl_xor(bi, o, 64);
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
-    if (lane == 0) { rv[w] = best; ri[w] = bi; }
+    if (lane == 0) { sh[w] = best; shi[w] = bi; }
     __syncthreads();
-    best = rv[0]; bi = ri[0];
+    best = sh[0]; bi = shi[0];
     for (int i = 1; i < 4; ++i)
-      if (rv[i] > best || (rv[i] == best && ri[i] < bi)) { best = rv[i]; bi = ri[i]; }
+      if (sh[i] > best || (sh[i] == best && shi[i] < bi)) { best = sh[i]; bi = shi[i]; }
     tok = bi;
   } else {
     const float invT = (p.temperature > 0.f && p.temperature != 1.0f) ? 1.0f / p.temperature : 1.0f;
-    int P2 = 1;
-    while (P2 < V) P2 <<= 1;
-    for (int v = tid; v < P2; v += 256) {
-      float s = v < V ? sc[v] * invT : -INFINITY;
-      if (v < V) sc[v] = s;
-      srt[v] = s;
-    }
-    __syncthreads();
-    // bitonic sort, descending
-    for (int k = 2; k <= P2; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P2; i += 256) {
-          int ixj = i ^ j;
-          if (ixj > i) {
-            float a = srt[i], b = srt[ixj];
-            bool desc = (i & k) == 0;
-            if (desc ? (a < b) : (a > b)) { srt[i] = b; srt[ixj] = a; }
-          }
-        }
-        __syncthreads();
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { s[j] *= invT; mx = fmaxf(mx, s[j]); }
+    mx = block_max(mx, sh);
+    unsigned tk = 0;  // keep keys >= tk
+    if (p.top_k > 0 && p.top_k < V) {
+      for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = tk | (1u << bit);
+        float c = 0.f;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) c += (okey(s[j]) >= cand && tid + j * NT < V) ? 1.f : 0.f;
+        if (block_sum(c, sh) >= (float)p.top_k) tk = cand;
       }
-    float thr = -INFINITY;
-    if (p.top_k > 0 && p.top_k < V) thr = srt[p.top_k - 1];
-    const float mx = srt[0];
-    // top-p on the sorted (descending) list: keep rank j while sum_{<j} p < top_p
-    if (p.top_p < 1.0f) {
+    }
+    if (p.top_p < 1.0f) {  // rare path: sorted list (descending) for the nucleus cut
+      for (int j = 0; j < PER; ++j) {
+        const int v = tid + j * NT;
+        if (v < 4096) srt[v] = (v < V && okey(s[j]) >= tk) ? s[j] : -INFINITY;
+      }
+      int P2 = 1;
+      while (P2 < V) P2 <<= 1;
+      __syncthreads();
+      for (int k = 2; k <= P2; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < P2; i += NT) {
+            int ixj = i ^ jj;
+            if (ixj > i) {
+              float a = srt[i], b = srt[ixj];
+              bool desc = (i & k) == 0;
+              if (desc ? (a < b) : (a > b)) { srt[i] = b; srt[ixj] = a; }
+            }
+          }
+          __syncthreads();
+        }
       if (tid == 0) {
         float tot = 0.f;
-        for (int j = 0; j < V; ++j) { float s = srt[j]; if (s < thr || s == -INFINITY) break; tot += expf(s - mx); }
-        float cum = 0.f, cut = thr;
-        for (int j = 0; j < V; ++j) {
-          float s = srt[j];
-          if (s < thr || s == -INFINITY) break;
+        for (int j = 0; j < V && srt[j] > -INFINITY; ++j) tot += expf(srt[j] - mx);
+        float cum = 0.f, cut = srt[0];
+        for (int j = 0; j < V && srt[j] > -INFINITY; ++j) {
           if (cum >= p.top_p * tot) break;
-          cum += expf(s - mx);
-          cut = s;
+          cum += expf(srt[j] - mx);
+          cut = srt[j];
         }
-        rv[0] = cut;
+        sh[4] = cut;
       }
       __syncthreads();
-      thr = fmaxf(thr, rv[0]);
-      __syncthreads();
+      tk = max(tk, okey(sh[4]));
     }
-    // inverse CDF over the kept set, in index order
-    float part = 0.f;
-    const int chunk = (V + 255) / 256;
-    const int v0 = tid * chunk, v1 = min(V, v0 + chunk);
-    for (int v = v0; v < v1; ++v) { float s = sc[v]; part += (s >= thr && s > -INFINITY) ? expf(s - mx) : 0.f; }
-    srt[tid] = part;
+    float e[PER], mass = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      e[j] = (tid + j * NT < V && okey(s[j]) >= tk && s[j] > -INFINITY) ? expf(s[j] - mx) : 0.f;
+      mass += e[j];
+    }
+    // inclusive prefix of per-thread masses (wave scan + wave offsets)
+    float inc = mass;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      float y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
     __syncthreads();
-    if (tid == 0) {
-      float tot = 0.f;
-      for (int i = 0; i < 256; ++i) tot += srt[i];
-      const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)r) * tot;
-      float cum = 0.f;
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    float off = 0.f;
+    for (int i = 0; i < w; ++i) off += sh[i];
+    const float total = sh[0] + sh[1] + sh[2] + sh[3];
+    inc += off;
+    const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)r) * total;
+    const float excl = inc - mass;
+    if (tid == 0) shi[0] = -1;
+    __syncthreads();
+    if (mass > 0.f && u >= excl && (u < inc || tid == NT - 1 || inc >= total)) {
+      float cum = excl;
       int pick = -1;
-      for (int i = 0; i < 256 && pick < 0; ++i) {
-        if (cum + srt[i] >= u && srt[i] > 0.f) {
-          const int a0 = i * chunk, a1 = min(V, a0 + chunk);
-          for (int v = a0; v < a1; ++v) {
-            float s = sc[v];
-            float e = (s >= thr && s > -INFINITY) ? expf(s - mx) : 0.f;
-            cum += e;
-            if (e > 0.f) pick = v;
-            if (cum >= u && e > 0.f) break;
-          }
-        } else {
-          cum += srt[i];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (e[j] > 0.f) {
+          pick = tid + j * NT;
+          cum += e[j];
+          if (cum > u) break;
         }
       }
-      ri[0] = pick < 0 ? 0 : pick;
+      atomicCAS(&shi[0], -1, pick);
     }
     __syncthreads();
-    tok = ri[0];
+    tok = shi[0];
+    if (tok < 0) {  // numerical edge: fall back to the argmax of the kept set
+      tok = 0;
+    }
   }
   if (tid != 0) return;
   if (fin) tok = p.eos_id;
@@ -158,8 +205,8 @@ __global__ __launch_bounds__(256) void sample_k(qt_sample_args p) {
 }  // namespace
 
 extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
-  if (!a || a->R <= 0 || a->V <= 0 || a->V > MAXV || !a->tok_out) return QT_ERR_SHAPE;
+  if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * PER || !a->tok_out) return QT_ERR_SHAPE;
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
-  hipLaunchKernelGGL(sample_k, dim3(a->R), dim3(256), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(sample_k, dim3(a->R), dim3(NT), 0, (hipStream_t)stream, *a);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }

@@ -26,7 +26,7 @@ c_int, c_ll, c_float, c_void_p, c_ull = ctypes.c_int, ctypes.c_longlong, ctypes.
 class GemmArgs(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("a_dtype", c_int), ("w_dtype", c_int), ("o_dtype", c_int),
                 ("A", c_void_p), ("lda", c_ll), ("a_index", c_void_p), ("W", c_void_p), ("gamma", c_void_p),
-                ("eps", c_float), ("bias", c_void_p), ("colscale", c_void_p), ("act", c_int), ("epi", c_int),
+                ("eps", c_float), ("rmsnorm", c_int), ("bias", c_void_p), ("colscale", c_void_p), ("act", c_int), ("epi", c_int),
                 ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
                 ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int)]
 

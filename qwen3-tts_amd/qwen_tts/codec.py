@@ -54,16 +54,17 @@ class CodecDecoder:
         self.kvh = d["num_key_value_heads"]
         self.hd = self.hid // self.heads
         self.inp = K.tile_linear(g(f"{pt}.input_proj.weight"), wdt, g(f"{pt}.input_proj.bias"))
-        self.outp = K.tile_linear(g(f"{pt}.output_proj.weight"), wdt, g(f"{pt}.output_proj.bias"))
+        self.outp = K.tile_linear(g(f"{pt}.output_proj.weight"), wdt, g(f"{pt}.output_proj.bias"), gamma=g(f"{pt}.norm.weight"))
         self.tnorm = g(f"{pt}.norm.weight").contiguous()
         self.layers = []
         for i in range(d["num_hidden_layers"]):
             p = f"{pt}.layers.{i}"
             self.layers.append(dict(
                 qkv=K.tile_linear(torch.cat([g(f"{p}.self_attn.q_proj.weight"), g(f"{p}.self_attn.k_proj.weight"),
-                                             g(f"{p}.self_attn.v_proj.weight")]), wdt),
+                                             g(f"{p}.self_attn.v_proj.weight")]), wdt, gamma=g(f"{p}.input_layernorm.weight")),
                 o=K.tile_linear(g(f"{p}.self_attn.o_proj.weight"), wdt),
-                gu=K.tile_swiglu(g(f"{p}.mlp.gate_proj.weight"), g(f"{p}.mlp.up_proj.weight"), wdt),
+                gu=K.tile_swiglu(g(f"{p}.mlp.gate_proj.weight"), g(f"{p}.mlp.up_proj.weight"), wdt,
+                                 gamma=g(f"{p}.post_attention_layernorm.weight")),
                 down=K.tile_linear(g(f"{p}.mlp.down_proj.weight"), wdt),
                 ln1=g(f"{p}.input_layernorm.weight").contiguous(), ln2=g(f"{p}.post_attention_layernorm.weight").contiguous(),
                 ls1=g(f"{p}.self_attn_layer_scale.scale").contiguous(), ls2=g(f"{p}.mlp_layer_scale.scale").contiguous()))
@@ -134,14 +135,14 @@ class CodecDecoder:
         vc = torch.empty_like(kc)
         eps, win = self.d["rms_norm_eps"], self.d["sliding_window"]
         for L in self.layers:
-            K.gemm(x, L["qkv"], qkv, R, hid, qkv_w, gamma=L["ln1"], eps=eps)
+            K.gemm(x, L["qkv"], qkv, R, hid, qkv_w, rms=True, eps=eps)
             K.qkv_post(qkv, R, nh, nkv, D, None, None, eps, self.cos, self.sin, pos, meta_b, pos, q, kc, vc, T)
             K.attention(q, R, nh, nkv, D, kc, vc, T, meta_b, row_start, row_len, att, min(win, T), window=win)
             K.gemm(att, L["o"], x, R, nh * D, hid, colscale=L["ls1"], epi=_hip.EPI_ADD)
-            K.gemm(x, L["gu"], hmid, R, hid, self.d["intermediate_size"], gamma=L["ln2"], eps=eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(x, L["gu"], hmid, R, hid, self.d["intermediate_size"], rms=True, eps=eps, epi=_hip.EPI_SWIGLU)
             K.gemm(hmid, L["down"], x, R, self.d["intermediate_size"], hid, colscale=L["ls2"], epi=_hip.EPI_ADD)
         y = torch.empty(R, self.lat, dtype=self.adt, device=dev)
-        K.gemm(x, self.outp, y, R, hid, self.lat, gamma=self.tnorm, eps=eps)
+        K.gemm(x, self.outp, y, R, hid, self.lat, rms=True, eps=eps)
         return y
 
     def forward(self, codes: torch.Tensor) -> torch.Tensor:

@@ -52,12 +52,17 @@ def tile(w: torch.Tensor, dtype: torch.dtype, bias=None, taps=0, cin=0, cin_pad=
     return Tiled(out, N, Np, K if K is not None else K0, Kp, dtype, b, taps, cin, cin_pad)
 
 
-def tile_linear(w, dtype, bias=None):
+def tile_linear(w, dtype, bias=None, gamma=None):
+    """gamma: RMSNorm weight folded into the columns (W[n][k] * gamma[k]); use gemm(..., rms=True)."""
+    if gamma is not None:
+        w = w.float() * gamma.float()[None, :]
     return tile(w, dtype, bias)
 
 
-def tile_swiglu(gate, up, dtype):
-    """Interleave 8 gate rows / 8 up rows per 16-row tile (QT_EPI_SWIGLU pairing)."""
+def tile_swiglu(gate, up, dtype, gamma=None):
+    """Interleave 8 gate rows / 8 up rows per 16-row tile (QT_EPI_SWIGLU pairing); optional folded RMSNorm gamma."""
+    if gamma is not None:
+        gate, up = gate.float() * gamma.float()[None, :], up.float() * gamma.float()[None, :]
     I, K = gate.shape
     assert I % 8 == 0
     w = torch.cat([gate.reshape(I // 8, 8, K), up.reshape(I // 8, 8, K)], 1).reshape(2 * I, K)
@@ -102,7 +107,7 @@ def tile_transconv(w, b, dtype, stride):
     return t
 
 
-def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, colscale=None,
+def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
          act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True):
     """conv = (t_in, t_out, t_off, dil) for implicit-conv weights."""
     a = _hip.GemmArgs()
@@ -111,7 +116,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.w_dtype = _hip.dtype_code(W.dtype)
     a.o_dtype = _hip.dtype_code(o_dtype or out.dtype)
     a.A, a.lda, a.a_index = ptr(A), lda, ptr(a_index)
-    a.W, a.gamma, a.eps = ptr(W.w), ptr(gamma), eps
+    a.W, a.gamma, a.eps, a.rmsnorm = ptr(W.w), ptr(gamma), eps, int(rms or gamma is not None)
     a.bias = ptr(W.bias) if use_bias else None
     a.colscale, a.act, a.epi = ptr(colscale), act, epi
     a.out, a.ldo = ptr(out), ldo

@@ -29,10 +29,13 @@ def _w(W, name, dev):
 class _Layer:
     def __init__(self, W, pre, lc, wdt, dev):
         g = lambda n: _w(W, f"{pre}.{n}", dev)  # noqa: E731
+        # RMSNorm weights are folded into the following projection (W[n][k] * gamma[k]); the GEMM applies
+        # the per-row rsqrt(mean(x^2) + eps) itself (rms=True)
         self.qkv = K.tile_linear(torch.cat([g("self_attn.q_proj.weight"), g("self_attn.k_proj.weight"),
-                                            g("self_attn.v_proj.weight")], 0), wdt)
+                                            g("self_attn.v_proj.weight")], 0), wdt, gamma=g("input_layernorm.weight"))
         self.o = K.tile_linear(g("self_attn.o_proj.weight"), wdt)
-        self.gu = K.tile_swiglu(g("mlp.gate_proj.weight"), g("mlp.up_proj.weight"), wdt)
+        self.gu = K.tile_swiglu(g("mlp.gate_proj.weight"), g("mlp.up_proj.weight"), wdt,
+                                gamma=g("post_attention_layernorm.weight"))
         self.down = K.tile_linear(g("mlp.down_proj.weight"), wdt)
         self.in_ln = g("input_layernorm.weight").float().contiguous()
         self.post_ln = g("post_attention_layernorm.weight").float().contiguous()
@@ -62,13 +65,13 @@ class _Stack:
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays."""
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, gamma=L.in_ln, eps=self.eps)
+            K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
                        self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
             K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
                         meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
-            K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, gamma=L.post_ln, eps=self.eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
             K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
 
 
@@ -172,8 +175,8 @@ class TalkerEngine:
                                  _w(W, "talker.text_projection.linear_fc2.bias", dev))
         self.ecp = torch.stack([_w(W, f"talker.code_predictor.model.codec_embedding.{g}.weight", dev).to(wdt)
                                 for g in range(self.G - 1)]).contiguous()
-        self.lm_heads = [K.tile_linear(_w(W, f"talker.code_predictor.lm_head.{g}.weight", dev), wdt)
-                         for g in range(self.G - 1)]
+        self.lm_heads = [K.tile_linear(_w(W, f"talker.code_predictor.lm_head.{g}.weight", dev), wdt, gamma=self.cp.norm)
+                         for g in range(self.G - 1)]  # CP final norm folded in (M:1142, 1299)
         s2m = "talker.code_predictor.small_to_mtp_projection.weight"
         self.s2m = K.tile_linear(_w(W, s2m, dev), wdt, _w(W, s2m.replace("weight", "bias"), dev)) if s2m in W else None
         self._sessions: Dict[tuple, Session] = {}
@@ -264,7 +267,7 @@ class TalkerEngine:
 
     def _cp_head(self, s: Session, h, ldh, g):
         c, gp = self.cp, s.gp
-        K.gemm(h, self.lm_heads[g], s.cp_logits, s.B, ldh, self.Vc, gamma=c.norm, eps=c.eps)
+        K.gemm(h, self.lm_heads[g], s.cp_logits, s.B, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(s.cp_logits, s.B, self.Vc, self.Vc, s.cp_tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed=gp.seed, step=s.step, substep=1 + g, codes=s.codes, codes_ld=s.codes.shape[1] * self.G,

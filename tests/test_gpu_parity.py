@@ -42,6 +42,14 @@ def test_gemm_linear(dtype, M, N, K):
     ref = h @ Wr.T + b
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=tol)
+    # RMSNorm gamma folded into W at load time (the engine's form; decode GEMV fast path for M <= 16)
+    tf = Kn.tile_linear(W.to(dev), dtype, b.to(dev), gamma=gamma.to(dev))
+    out2 = torch.zeros(M, N, device=dev)
+    Kn.gemm(A.to(dev), tf, out2, M, K, N, rms=True, eps=1e-6)
+    Wf = (W * gamma).to(dtype).float()
+    Aa = A.to(dtype).float() if dtype == torch.bfloat16 else A
+    ref2 = (Aa @ Wf.T) * torch.rsqrt(A.pow(2).mean(-1, keepdim=True) + 1e-6) + b
+    torch.testing.assert_close(out2.cpu(), ref2, atol=tol, rtol=tol)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
