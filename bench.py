@@ -94,7 +94,11 @@ def kernel_roofline(tts, ids, languages, speakers, frames):
     eng = tts.model.engine
 
     def on_frames(s, n):
-        started["on"] = n >= 1  # skip the prefill; record the decode frames
+        # skip the prefill; before the recorded frames are enqueued, park the GPU on a spin kernel so the
+        # host (ctypes launches) runs ahead and the events time back-to-back kernels, not enqueue gaps
+        if n == 1:
+            torch.cuda._sleep(int(3e8))
+        started["on"] = n >= 1
 
     Kn.gemm = hooked
     try:

@@ -101,6 +101,23 @@ typedef struct qt_attn_args {
 int qt_attention(const qt_attn_args* args, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * qt_decode_attention: qt_qkv_post + qt_attention fused for rows whose key range ends at their own new
+ * position (talker / code-predictor decode, M:773-801): per (row, kv head) q/k RMSNorm + RoPE, append of
+ * the new k/v at kv_pos[r], then attention over keys [max(row_start[r], kv_pos[r]+1-window), kv_pos[r]].
+ * out fp32 [R][Hq*D].  Rows must not read each other's new keys (one row per batch entry).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_decode_attn_args {
+  int R, Hq, Hkv, D, Lmax, window;
+  const float* qkv;
+  const float* q_norm; const float* k_norm; float eps;
+  const float* cos_tab; const float* sin_tab;
+  const int* rope_pos; const int* row_batch; const int* kv_pos; const int* row_start;
+  void* k_cache; void* v_cache; int kv_dtype;
+  float* out;
+} qt_decode_attn_args;
+int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * qt_sample: transformers-4.57 logits processing + token choice, one row per block.
  * RepetitionPenalty (seen flags) -> MinNewTokens (mask eos while *n_generated < min_new_tokens) ->
  * SuppressTokens [suppress_lo, suppress_hi) except suppress_keep (+ eos when ignore_eos) ->

@@ -186,6 +186,173 @@ int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Fused decode attention: one 1024-thread block per (query row, kv head).  Waves 0..NREP+1 first apply
+// q/k RMSNorm + RoPE to this block's NREP query heads and its kv head's new key, append k/v to the cache
+// at kv_pos (the new key itself is served from LDS, so no intra-launch global read-after-write), then all
+// 16 waves stream the cached keys: lane group g (D/8 lanes, 16 B bf16 per lane) owns keys g, g+G, ...;
+// K and V fragments of IC keys are loaded before any use (IC x 2 KiB in flight per group) and folded
+// into an online softmax; partial (m, l, o) merge across groups by shuffles and across waves via LDS.
+// Bytes per (row, head) = 2 * L * D * sizeof(kv): the decode-attention HBM roofline of SURVEY.md §8(d).
+template <typename KV, int D, int NREP>
+__global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
+  constexpr int LPK = D / 8, GPW = 64 / LPK, G = 16 * GPW, IC = 4;
+  __shared__ float qs[NREP][D];
+  __shared__ float knew[D], vnew[D];
+  __shared__ float mrg_ml[16][NREP][2];
+  __shared__ float mrg_o[16][NREP][D];
+  const int r = blockIdx.x, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int half = D / 2;
+  const int nq = p.Hq, nk = p.Hkv;
+  const int b = p.row_batch[r];
+  const int kvpos = p.kv_pos[r];
+  const long long base = ((long long)b * nk + h) * p.Lmax * D;
+  // ---- phase 0: norm + rope of q heads / new k, v passthrough; append to cache
+  if (w < NREP + 2) {
+    const int hh = w < NREP ? h * NREP + w : (w == NREP ? nq + h : nq + nk + h);
+    const float* src = p.qkv + (long long)r * (nq + 2 * nk) * D + (long long)hh * D;
+    const bool act = lane < half;
+    float x0 = act ? src[lane] : 0.f, x1 = act ? src[lane + half] : 0.f;
+    if (w <= NREP) {
+      const float* nw = w < NREP ? p.q_norm : p.k_norm;
+      if (nw) {
+        const float rs = rsqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + p.eps);
+        if (act) { x0 = nw[lane] * (x0 * rs); x1 = nw[lane + half] * (x1 * rs); }
+      }
+      const int pos = p.rope_pos[r];
+      if (act) {
+        const float c = p.cos_tab[(long long)pos * half + lane], sn = p.sin_tab[(long long)pos * half + lane];
+        const float y0 = x0 * c - x1 * sn, y1 = x1 * c + x0 * sn;
+        x0 = y0; x1 = y1;
+      }
+    }
+    if (act) {
+      float* dst = w < NREP ? qs[w] : (w == NREP ? knew : vnew);
+      if (w >= NREP) {  // the new key/value as the cache will hold them (kv dtype rounding)
+        x0 = to_f(from_f<KV>(x0));
+        x1 = to_f(from_f<KV>(x1));
+      }
+      dst[lane] = x0; dst[lane + half] = x1;
+      if (w >= NREP) {
+        KV* cache = (KV*)(w == NREP ? p.k_cache : p.v_cache) + base + (long long)kvpos * D;
+        cache[lane] = from_f<KV>(x0);
+        cache[lane + half] = from_f<KV>(x1);
+      }
+    }
+  }
+  __syncthreads();
+  const int grp = lane / LPK, sub = lane % LPK;
+  const int gid = w * GPW + grp;
+  int start = p.row_start[r];
+  const int len = kvpos + 1;
+  if (p.window > 0) start = max(start, len - p.window);
+  const int n = len - start;  // keys [start, len); the last one (kvpos) comes from LDS
+  const float scale = rsqrtf((float)D);
+  float q[NREP][8];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[j][i] = qs[j][sub * 8 + i] * scale;
+  float m[NREP], l[NREP], o[NREP][8];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j) {
+    m[j] = -INFINITY; l[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[j][i] = 0.f;
+  }
+  const KV* Kc = (const KV*)p.k_cache + base;
+  const KV* Vc = (const KV*)p.v_cache + base;
+  for (int j0 = gid; j0 < n; j0 += G * IC) {
+    float kf[IC][8], vf[IC][8];
+#pragma unroll
+    for (int c = 0; c < IC; ++c) {
+      const int jj = j0 + c * G;
+      const int t = start + min(jj, n - 1);
+      if (jj < n - 1) {
+        load8f(Kc + (long long)t * D + sub * 8, kf[c]);
+        load8f(Vc + (long long)t * D + sub * 8, vf[c]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { kf[c][i] = knew[sub * 8 + i]; vf[c][i] = vnew[sub * 8 + i]; }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < IC; ++c) {
+      const bool valid = j0 + c * G < n;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d += q[j][i] * kf[c][i];
+#pragma unroll
+        for (int off = LPK / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+        if (valid) {
+          const float mn = fmaxf(m[j], d);
+          const float f = expf(m[j] - mn), e = expf(d - mn);
+          l[j] = l[j] * f + e;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vf[c][i];
+          m[j] = mn;
+        }
+      }
+    }
+  }
+  // merge lane groups inside the wave
+#pragma unroll
+  for (int off = LPK; off < 64; off <<= 1) {
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const float m2 = __shfl_xor(m[j], off, 64), l2 = __shfl_xor(l[j], off, 64);
+      const float mn = fmaxf(m[j], m2);
+      const float f1 = m[j] == -INFINITY ? 0.f : expf(m[j] - mn);
+      const float f2 = m2 == -INFINITY ? 0.f : expf(m2 - mn);
+      l[j] = l[j] * f1 + l2 * f2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float o2 = __shfl_xor(o[j][i], off, 64);
+        o[j][i] = o[j][i] * f1 + o2 * f2;
+      }
+      m[j] = mn;
+    }
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      if (sub == 0) { mrg_ml[w][j][0] = m[j]; mrg_ml[w][j][1] = l[j]; }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mrg_o[w][j][sub * 8 + i] = o[j][i];
+    }
+  }
+  __syncthreads();
+  if (tid < NREP * D) {
+    const int j = tid / D, d = tid % D;
+    float mm = -INFINITY;
+    for (int ww = 0; ww < 16; ++ww) mm = fmaxf(mm, mrg_ml[ww][j][0]);
+    float ll = 0.f, oo = 0.f;
+    for (int ww = 0; ww < 16; ++ww) {
+      const float mw = mrg_ml[ww][j][0];
+      const float f = mw == -INFINITY ? 0.f : expf(mw - mm);
+      ll += mrg_ml[ww][j][1] * f;
+      oo += mrg_o[ww][j][d] * f;
+    }
+    ((float*)p.out)[((long long)r * nq + h * NREP + j) * D + d] = oo / ll;
+  }
+}
+
+template <typename KV, int D>
+int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
+  dim3 g(a.R, a.Hkv);
+  switch (a.Hq / a.Hkv) {
+    case 1: hipLaunchKernelGGL((attn_decode_k<KV, D, 1>), g, dim3(1024), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((attn_decode_k<KV, D, 2>), g, dim3(1024), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4>), g, dim3(1024), 0, s, a); break;
+    default: return QT_ERR_SHAPE;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
 }  // namespace
 
 extern "C" int qt_qkv_post(const qt_qkv_args* a, void* stream) {
@@ -207,4 +374,17 @@ extern "C" int qt_attention(const qt_attn_args* a, void* stream) {
   if (a->kv_dtype == QT_BF16 && a->o_dtype == QT_BF16) return attn_dispatch<bf16_t, bf16_t>(*a, s);
   if (a->kv_dtype == QT_F32 && a->o_dtype == QT_F32) return attn_dispatch<float, float>(*a, s);
   return QT_ERR_DTYPE;
+}
+
+extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
+  if (!a || a->R <= 0 || a->Hkv <= 0 || a->Hq % a->Hkv) return QT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = a->kv_dtype == QT_BF16;
+  if (!bf && a->kv_dtype != QT_F32) return QT_ERR_DTYPE;
+  switch (a->D) {
+    case 16: return bf ? decode_dispatch<bf16_t, 16>(*a, s) : decode_dispatch<float, 16>(*a, s);
+    case 64: return bf ? decode_dispatch<bf16_t, 64>(*a, s) : decode_dispatch<float, 64>(*a, s);
+    case 128: return bf ? decode_dispatch<bf16_t, 128>(*a, s) : decode_dispatch<float, 128>(*a, s);
+    default: return QT_ERR_SHAPE;
+  }
 }

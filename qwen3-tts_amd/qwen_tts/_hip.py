@@ -45,6 +45,14 @@ class AttnArgs(ctypes.Structure):
                 ("o_dtype", c_int), ("max_keys", c_int)]
 
 
+class DecodeAttnArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("Lmax", c_int), ("window", c_int),
+                ("qkv", c_void_p), ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float),
+                ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("row_batch", c_void_p),
+                ("kv_pos", c_void_p), ("row_start", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
+                ("kv_dtype", c_int), ("out", c_void_p)]
+
+
 class SampleArgs(ctypes.Structure):
     _fields_ = [("logits", c_void_p), ("R", c_int), ("V", c_int), ("ld", c_ll), ("seen", c_void_p),
                 ("rep_penalty", c_float), ("n_generated", c_void_p), ("min_new_tokens", c_int), ("eos_id", c_int),
@@ -55,7 +63,7 @@ class SampleArgs(ctypes.Structure):
                 ("codes_col", c_int), ("codes_step_off", c_int)]
 
 
-EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_sample", "qt_rmsnorm", "qt_gather_rows",
+EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_sample", "qt_rmsnorm", "qt_gather_rows",
            "qt_frame_embed", "qt_advance", "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
 
 _LIB = None
@@ -70,7 +78,7 @@ def load_library(path: str = LIB_PATH):
     P = c_void_p
     sig = {
         "qt_gemm": [P, P], "qt_tile_weight": [P, c_int, c_int, c_int, P, P], "qt_qkv_post": [P, P],
-        "qt_attention": [P, P], "qt_sample": [P, P],
+        "qt_attention": [P, P], "qt_decode_attention": [P, P], "qt_sample": [P, P],
         "qt_rmsnorm": [P, P, c_float, P, c_int, c_int, P],
         "qt_gather_rows": [P, c_int, P, c_int, c_int, P, c_ll, P],
         "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, c_int, P],

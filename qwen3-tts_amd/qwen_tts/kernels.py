@@ -146,6 +146,17 @@ def attention(q, R, Hq, Hkv, D, kc, vc, Lmax, row_batch, row_start, row_len, out
     check(_hip.lib().qt_attention(ctypes.byref(a), stream()), "qt_attention")
 
 
+def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, row_start,
+                     kc, vc, Lmax, out, window=0):
+    a = _hip.DecodeAttnArgs()
+    a.R, a.Hq, a.Hkv, a.D, a.Lmax, a.window = R, Hq, Hkv, D, Lmax, window
+    a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    a.rope_pos, a.row_batch, a.kv_pos, a.row_start = ptr(rope_pos), ptr(row_batch), ptr(kv_pos), ptr(row_start)
+    a.k_cache, a.v_cache, a.kv_dtype, a.out = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype), ptr(out)
+    check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
+
+
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,

@@ -61,15 +61,21 @@ class _Stack:
         if self.cos.shape[0] < npos:
             self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
 
-    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys):
-        """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays."""
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False):
+        """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
+        decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention."""
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
             K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
-            K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
-                       self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
-            K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
-                        meta["row_start"], meta["row_len"], scratch["att"], max_keys)
+            if decode:
+                K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
+                                   self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
+                                   meta["row_start"], kc, vc, Lmax, scratch["att"])
+            else:
+                K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
+                           self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
+                K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
+                            meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
             K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
             K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
@@ -254,12 +260,12 @@ class TalkerEngine:
                 K.gemm(self.ecp[g - 1], self.s2m, x, B, t.H, Hc, a_dtype=self.ecp.dtype, a_index=s.cp_tok)
             else:
                 K.gather_rows(self.ecp[g - 1], s.cp_tok, B, Hc, x, Hc)
-            c.forward(x, B, s.cp_meta[g - 1], s.cp_kv, s.sc_c, s.cp_L, s.cp_L)
+            c.forward(x, B, s.cp_meta[g - 1], s.cp_kv, s.sc_c, s.cp_L, s.cp_L, decode=True)
             self._cp_head(s, x, Hc, g)
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B)
-        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax)
+        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True)
         K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
         self._sample_talker(s, s.logits, 1, 0)

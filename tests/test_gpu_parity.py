@@ -156,6 +156,36 @@ def test_qkv_post_and_attention(D, hq, hkv, window):
     torch.testing.assert_close(att.cpu(), ref, atol=2e-5, rtol=2e-5)
 
 
+@pytest.mark.parametrize("D,hq,hkv,L", [(128, 16, 8, 300), (128, 16, 8, 17), (16, 4, 2, 9)])
+@pytest.mark.parametrize("kvdt", [torch.float32, torch.bfloat16])
+def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
+    """Fused qt_decode_attention == qt_qkv_post + qt_attention on the same cache (decode rows)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(L + D)
+    B = 4
+    qkv = torch.randn(B, (hq + 2 * hkv) * D, generator=g).to(dev)
+    qn, kn = (1 + 0.1 * torch.randn(D, generator=g)).to(dev), (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    kc = torch.randn(B, hkv, L + 3, D, generator=g).to(dev, kvdt)
+    vc = torch.randn(B, hkv, L + 3, D, generator=g).to(dev, kvdt)
+    kc2, vc2 = kc.clone(), vc.clone()
+    cos, sin = Kn.rope_tables(D, 1e6, L + 64, dev)
+    i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
+    pos, kvpos = i32([L - 1 + 5, L - 1, L - 1 + 2, L - 1]), i32([L - 1] * B)
+    rb, start = i32(range(B)), i32([0, 3, 0, L - 1])
+    q = torch.zeros(B, hq * D, device=dev)
+    a1 = torch.zeros(B, hq * D, device=dev)
+    Kn.qkv_post(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, kvpos, q, kc, vc, L + 3)
+    Kn.attention(q, B, hq, hkv, D, kc, vc, L + 3, rb, start, kvpos + 1, a1, L)
+    a2 = torch.zeros(B, hq * D, device=dev)
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, kvpos, start, kc2, vc2, L + 3, a2)
+    ktol = 2e-6 if kvdt == torch.float32 else 1e-2  # fp contraction / one bf16 ulp
+    torch.testing.assert_close(kc2.float(), kc.float(), atol=ktol, rtol=ktol)
+    torch.testing.assert_close(vc2.float(), vc.float(), atol=0, rtol=0)
+    tol = 2e-5 if kvdt == torch.float32 else 2e-3
+    torch.testing.assert_close(a2, a1, atol=tol, rtol=tol)
+
+
 def test_sample_greedy_processors():
     from qwen_tts import kernels as Kn
     from oracle.talker import process_logits
