@@ -36,17 +36,17 @@ def synth_ids(n, seed):
 
 
 def make_weights(preset, dev, world, rank):
-    import torch.distributed as dist
     from qwen_tts.weights import codec_specs, read_json, resolve_path, synthetic, talker_specs
     d = resolve_path(f"synthetic:{preset}")
     cfg = read_json(os.path.join(d, "config.json"))
     ccfg = read_json(os.path.join(d, "speech_tokenizer", "config.json"))
     specs_t, specs_c = talker_specs(cfg), codec_specs(ccfg)
     if world > 1:  # rank 0 generates, RCCL broadcast over xGMI (the only collective of the design)
+        from qwen_tts.dp import broadcast_weights
         W = synthetic(specs_t, dev) if rank == 0 else {n: torch.empty(s, device=dev) for n, s in specs_t}
         CW = synthetic(specs_c, dev) if rank == 0 else {n: torch.empty(s, device=dev) for n, s in specs_c}
-        for t in list(W.values()) + list(CW.values()):
-            dist.broadcast(t, 0)
+        broadcast_weights(W)
+        broadcast_weights(CW)
     else:
         W, CW = synthetic(specs_t, dev), synthetic(specs_c, dev)
     return cfg, W, CW
@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--preset", default="1.7b-customvoice")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--cpu-frames", type=int, default=24)
     ap.add_argument("--roofline", type=int, default=1)
     a = ap.parse_args()
 
@@ -199,13 +199,9 @@ def main():
         lat.append(s_t)
     barrier()
     dt = time.perf_counter() - t0
-    tt = torch.tensor([dt, audio], dtype=torch.float64, device=dev)
     if dist is not None:
-        mx = tt[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt[1:].clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        dt, audio = float(mx), float(sm)
+        from qwen_tts.dp import reduce_timing
+        dt, audio = reduce_timing(dt, audio, device=dev)
     value = audio / dt
     roof = None
     if a.roofline and rank == 0:

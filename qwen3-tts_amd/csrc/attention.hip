@@ -209,6 +209,24 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
   const int b = p.row_batch[r];
   const int kvpos = p.kv_pos[r];
   const long long base = ((long long)b * nk + h) * p.Lmax * D;
+  const int grp = lane / LPK, sub = lane % LPK;
+  const int gid = w * GPW + grp;
+  int start = p.row_start[r];
+  const int len = kvpos + 1;
+  if (p.window > 0) start = max(start, len - p.window);
+  const int n = len - start;  // keys [start, len); the last one (kvpos) comes from LDS
+  const KV* Kc = (const KV*)p.k_cache + base;
+  const KV* Vc = (const KV*)p.v_cache + base;
+  float kf[IC][8], vf[IC][8];
+  auto load_chunk = [&](int j0) {  // cached keys only; the new key's slot is filled after phase 0
+#pragma unroll
+    for (int c = 0; c < IC; ++c) {
+      const int jj = min(j0 + c * G, max(n - 2, 0));
+      load8f(Kc + (long long)(start + jj) * D + sub * 8, kf[c]);
+      load8f(Vc + (long long)(start + jj) * D + sub * 8, vf[c]);
+    }
+  };
+  if (gid < n) load_chunk(gid);  // in flight while phase 0 runs
   // ---- phase 0: norm + rope of q heads / new k, v passthrough; append to cache
   if (w < NREP + 2) {
     const int hh = w < NREP ? h * NREP + w : (w == NREP ? nq + h : nq + nk + h);
@@ -243,12 +261,6 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
     }
   }
   __syncthreads();
-  const int grp = lane / LPK, sub = lane % LPK;
-  const int gid = w * GPW + grp;
-  int start = p.row_start[r];
-  const int len = kvpos + 1;
-  if (p.window > 0) start = max(start, len - p.window);
-  const int n = len - start;  // keys [start, len); the last one (kvpos) comes from LDS
   const float scale = rsqrtf((float)D);
   float q[NREP][8];
 #pragma unroll
@@ -262,18 +274,10 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[j][i] = 0.f;
   }
-  const KV* Kc = (const KV*)p.k_cache + base;
-  const KV* Vc = (const KV*)p.v_cache + base;
   for (int j0 = gid; j0 < n; j0 += G * IC) {
-    float kf[IC][8], vf[IC][8];
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
-      const int jj = j0 + c * G;
-      const int t = start + min(jj, n - 1);
-      if (jj < n - 1) {
-        load8f(Kc + (long long)t * D + sub * 8, kf[c]);
-        load8f(Vc + (long long)t * D + sub * 8, vf[c]);
-      } else {
+      if (j0 + c * G >= n - 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) { kf[c][i] = knew[sub * 8 + i]; vf[c][i] = vnew[sub * 8 + i]; }
       }
@@ -298,6 +302,7 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
         }
       }
     }
+    if (j0 + G * IC < n) load_chunk(j0 + G * IC);
   }
   // merge lane groups inside the wave
 #pragma unroll

@@ -192,6 +192,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[mrow] : (long long)mrow) * p.lda + lk * E;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
+  // epilogue operands of wave 0 issued before the weight stream (hides one dependent round trip)
+  const int n = nt * 16 + lm;
+  const bool nval = n < p.N;
+  float pre_bias = 0.f, pre_cs = 1.f, pre_out[4] = {0.f, 0.f, 0.f, 0.f};
+  if (w == 0) {
+    if (p.bias && nval) pre_bias = p.bias[n];
+    if (p.colscale && nval) pre_cs = p.colscale[n];
+    if (p.epi == QT_EPI_ADD && nval) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (lk * 4 + i < p.M) pre_out[i] = to_f(((const OT*)p.out)[(long long)(lk * 4 + i) * p.ldo + n]);
+    }
+  }
   const WT* wp = (const WT*)p.W + ((size_t)nt * ktiles) * 64 * E + lane * E;
   for (int c = kt0; c < kt1; c += U) {
     u32x4_t wv[U];
@@ -236,10 +249,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   for (int ww = 0; ww < WPB; ++ww) {
     v[0] += red[ww][lane][0]; v[1] += red[ww][lane][1]; v[2] += red[ww][lane][2]; v[3] += red[ww][lane][3];
   }
-  const int n = nt * 16 + lm;
-  const bool nval = n < p.N;
-  const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
-  const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
+  const float bias = pre_bias, cs = pre_cs;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float x = v[i];
@@ -270,7 +280,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     const int m = lk * 4 + i;
     if (m >= p.M || !nval) continue;
     OT* o = out + (long long)m * p.ldo + n;
-    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[i]);
+    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(pre_out[i] + v[i]);
     else *o = from_f<OT>(v[i]);
   }
 }

@@ -28,19 +28,31 @@ __global__ void gather_rows_k(const T* __restrict__ tab, const int* __restrict__
 }
 
 template <typename ET>
-__global__ void frame_embed_k(const ET* __restrict__ e0, const ET* __restrict__ ecp, int V0, int Vcp, int G, int H,
-                              const int* __restrict__ codes, long long codes_ld, const int* __restrict__ step,
-                              const float* __restrict__ trailing, int T, const float* __restrict__ pad,
-                              float* __restrict__ x) {  // ET: table dtype
+__global__ __launch_bounds__(256) void frame_embed_k(const ET* __restrict__ e0, const ET* __restrict__ ecp, int V0,
+                                                     int Vcp, int G, int H, const int* __restrict__ codes,
+                                                     long long codes_ld, const int* __restrict__ step,
+                                                     const float* __restrict__ trailing, int T,
+                                                     const float* __restrict__ pad, float* __restrict__ x) {
+  // ET: table dtype.  Codes to LDS once, then every thread issues its 16 row-slice loads before summing.
+  __shared__ int cs[32];
   const int b = blockIdx.x;
   const int t = *step;
-  const int* c = codes + (long long)b * codes_ld + (long long)t * G;
+  if (threadIdx.x < G) cs[threadIdx.x] = codes[(long long)b * codes_ld + (long long)t * G + threadIdx.x];
+  __syncthreads();
   const float* tr = t < T ? trailing + ((long long)b * T + t) * H : pad;
-  for (int i = threadIdx.x; i < H; i += blockDim.x) {
-    // sum order: cat([...16 codebooks]).sum(1) then + text (M:1681-1692)
-    float s = to_f(e0[(long long)c[0] * H + i]);
-    for (int g = 1; g < G; ++g) s += to_f(ecp[((long long)(g - 1) * Vcp + c[g]) * H + i]);
-    x[(long long)b * H + i] = s + tr[i];
+  for (int i = threadIdx.x * 8; i < H; i += blockDim.x * 8) {
+    float acc[8], v[8];
+    load8f(e0 + (long long)cs[0] * H + i, acc);
+    for (int g = 1; g < G; ++g) {  // sum order: cat([...16 codebooks]).sum(1) then + text (M:1681-1692)
+      load8f(ecp + ((long long)(g - 1) * Vcp + cs[g]) * H + i, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    load8f(tr + i, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    store4(x + (long long)b * H + i, acc);
+    store4(x + (long long)b * H + i + 4, acc + 4);
   }
 }
 
@@ -150,7 +162,7 @@ extern "C" int qt_gather_rows(const void* tab, int dtype, const int* idx, int M,
 extern "C" int qt_frame_embed(const void* e0, const void* ecp, int dtype, int V0, int Vcp, int G, int H,
                               const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
                               const float* pad, float* x, int B, void* s) {
-  if (B <= 0 || H <= 0 || G < 1) return QT_ERR_SHAPE;
+  if (B <= 0 || H <= 0 || G < 1 || G > 32 || H % 8) return QT_ERR_SHAPE;
   if (dtype == QT_BF16)
     hipLaunchKernelGGL(frame_embed_k<bf16_t>, dim3(B), dim3(256), 0, (hipStream_t)s, (const bf16_t*)e0,
                        (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x);

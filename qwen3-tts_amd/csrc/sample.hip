@@ -58,6 +58,7 @@ QT_DEV float block_max(float v, float* sh) {
 __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
   __shared__ float sh[8];
   __shared__ int shi[4];
+  __shared__ int cntk[2][4];
   __shared__ float srt[4096];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = p.V;
@@ -106,12 +107,18 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
     mx = block_max(mx, sh);
     unsigned tk = 0;  // keep keys >= tk
     if (p.top_k > 0 && p.top_k < V) {
+      unsigned key[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) key[j] = (tid + j * NT < V) ? okey(s[j]) : 0u;
+      // MSB-first construction of the k-th largest key: one ballot count + one barrier per bit
       for (int bit = 31; bit >= 0; --bit) {
         const unsigned cand = tk | (1u << bit);
-        float c = 0.f;
+        int c = 0;
 #pragma unroll
-        for (int j = 0; j < PER; ++j) c += (okey(s[j]) >= cand && tid + j * NT < V) ? 1.f : 0.f;
-        if (block_sum(c, sh) >= (float)p.top_k) tk = cand;
+        for (int j = 0; j < PER; ++j) c += __popcll(__ballot(key[j] >= cand));
+        if (lane == 0) cntk[bit & 1][w] = c;
+        __syncthreads();
+        if (cntk[bit & 1][0] + cntk[bit & 1][1] + cntk[bit & 1][2] + cntk[bit & 1][3] >= p.top_k) tk = cand;
       }
     }
     if (p.top_p < 1.0f) {  // rare path: sorted list (descending) for the nucleus cut
