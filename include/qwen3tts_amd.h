@@ -60,7 +60,12 @@ typedef struct qt_gemm_args {
   void* out;
   long long ldo;
   int taps, dil, cin, cin_pad, t_in, t_out, t_off;
+  /* decode GEMV (M<=16) split-K: ws = zero-initialised device scratch of ws_bytes (>= QT_GEMM_WS_MIN),
+   * owned by the caller and used by one stream at a time; splitk 0 = auto, 1 = off, n = force n.
+   * Partials are reduced in a fixed order by the last-arriving block: results are deterministic. */
+  void* ws; long long ws_bytes; int splitk;
 } qt_gemm_args;
+#define QT_GEMM_WS_MIN (4 << 20)
 
 int qt_gemm(const qt_gemm_args* args, void* stream);
 

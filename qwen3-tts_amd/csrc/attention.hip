@@ -188,20 +188,21 @@ int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------------------------
-// Fused decode attention: one 1024-thread block per (query row, kv head).  Waves 0..NREP+1 first apply
+// Fused decode attention: one 512-thread block per (query row, kv head).  Waves 0..NREP+1 first apply
 // q/k RMSNorm + RoPE to this block's NREP query heads and its kv head's new key, append k/v to the cache
 // at kv_pos (the new key itself is served from LDS, so no intra-launch global read-after-write), then all
-// 16 waves stream the cached keys: lane group g (D/8 lanes, 16 B bf16 per lane) owns keys g, g+G, ...;
+// 8 waves stream the cached keys: lane group g (D/8 lanes, 16 B bf16 per lane) owns keys g, g+G, ...;
 // K and V fragments of IC keys are loaded before any use (IC x 2 KiB in flight per group) and folded
 // into an online softmax; partial (m, l, o) merge across groups by shuffles and across waves via LDS.
 // Bytes per (row, head) = 2 * L * D * sizeof(kv): the decode-attention HBM roofline of SURVEY.md §8(d).
 template <typename KV, int D, int NREP>
-__global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
-  constexpr int LPK = D / 8, GPW = 64 / LPK, G = 16 * GPW, IC = 4;
+__global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
+  constexpr int NW = 8;  // waves: 8 x 64 lanes keeps kf/vf/o/q (~150 VGPRs) out of scratch
+  constexpr int LPK = D / 8, GPW = 64 / LPK, G = NW * GPW, IC = 4;
   __shared__ float qs[NREP][D];
   __shared__ float knew[D], vnew[D];
-  __shared__ float mrg_ml[16][NREP][2];
-  __shared__ float mrg_o[16][NREP][D];
+  __shared__ float mrg_ml[NW][NREP][2];
+  __shared__ float mrg_o[NW][NREP][D];
   const int r = blockIdx.x, h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int half = D / 2;
@@ -217,13 +218,30 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
   const int n = len - start;  // keys [start, len); the last one (kvpos) comes from LDS
   const KV* Kc = (const KV*)p.k_cache + base;
   const KV* Vc = (const KV*)p.v_cache + base;
-  float kf[IC][8], vf[IC][8];
+  // raw fragments stay packed (bf16: 4 VGPRs per 8 elements) until used: IC keys in flight per group
+  constexpr int RW = sizeof(KV) * 8 / 4;  // 32-bit words per 8-element fragment
+  unsigned kr[IC][RW], vr[IC][RW];
   auto load_chunk = [&](int j0) {  // cached keys only; the new key's slot is filled after phase 0
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
       const int jj = min(j0 + c * G, max(n - 2, 0));
-      load8f(Kc + (long long)(start + jj) * D + sub * 8, kf[c]);
-      load8f(Vc + (long long)(start + jj) * D + sub * 8, vf[c]);
+      const unsigned* ks = (const unsigned*)(Kc + (long long)(start + jj) * D + sub * 8);
+      const unsigned* vs = (const unsigned*)(Vc + (long long)(start + jj) * D + sub * 8);
+#pragma unroll
+      for (int q4 = 0; q4 < RW; q4 += 4) {
+        u32x4_t a = *(const u32x4_t*)(ks + q4), b = *(const u32x4_t*)(vs + q4);
+        kr[c][q4] = a[0]; kr[c][q4 + 1] = a[1]; kr[c][q4 + 2] = a[2]; kr[c][q4 + 3] = a[3];
+        vr[c][q4] = b[0]; vr[c][q4 + 1] = b[1]; vr[c][q4 + 2] = b[2]; vr[c][q4 + 3] = b[3];
+      }
+    }
+  };
+  auto unpack = [&](const unsigned* r, float* o8) {
+    if constexpr (sizeof(KV) == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { o8[2 * i] = __uint_as_float(r[i] << 16); o8[2 * i + 1] = __uint_as_float(r[i] & 0xFFFF0000u); }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o8[i] = __uint_as_float(r[i]);
     }
   };
   if (gid < n) load_chunk(gid);  // in flight while phase 0 runs
@@ -277,19 +295,19 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
   for (int j0 = gid; j0 < n; j0 += G * IC) {
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
+      const bool valid = j0 + c * G < n;
+      float kf[8], vf[8];
+      unpack(kr[c], kf);
+      unpack(vr[c], vf);
       if (j0 + c * G >= n - 1) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { kf[c][i] = knew[sub * 8 + i]; vf[c][i] = vnew[sub * 8 + i]; }
+        for (int i = 0; i < 8; ++i) { kf[i] = knew[sub * 8 + i]; vf[i] = vnew[sub * 8 + i]; }
       }
-    }
-#pragma unroll
-    for (int c = 0; c < IC; ++c) {
-      const bool valid = j0 + c * G < n;
 #pragma unroll
       for (int j = 0; j < NREP; ++j) {
         float d = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) d += q[j][i] * kf[c][i];
+        for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
 #pragma unroll
         for (int off = LPK / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
         if (valid) {
@@ -297,7 +315,7 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
           const float f = expf(m[j] - mn), e = expf(d - mn);
           l[j] = l[j] * f + e;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vf[c][i];
+          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vf[i];
           m[j] = mn;
         }
       }
@@ -331,12 +349,12 @@ __global__ __launch_bounds__(1024) void attn_decode_k(qt_decode_attn_args p) {
     }
   }
   __syncthreads();
-  if (tid < NREP * D) {
-    const int j = tid / D, d = tid % D;
+  for (int e = tid; e < NREP * D; e += NW * 64) {
+    const int j = e / D, d = e % D;
     float mm = -INFINITY;
-    for (int ww = 0; ww < 16; ++ww) mm = fmaxf(mm, mrg_ml[ww][j][0]);
+    for (int ww = 0; ww < NW; ++ww) mm = fmaxf(mm, mrg_ml[ww][j][0]);
     float ll = 0.f, oo = 0.f;
-    for (int ww = 0; ww < 16; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
       const float mw = mrg_ml[ww][j][0];
       const float f = mw == -INFINITY ? 0.f : expf(mw - mm);
       ll += mrg_ml[ww][j][1] * f;
@@ -350,9 +368,9 @@ template <typename KV, int D>
 int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
   dim3 g(a.R, a.Hkv);
   switch (a.Hq / a.Hkv) {
-    case 1: hipLaunchKernelGGL((attn_decode_k<KV, D, 1>), g, dim3(1024), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((attn_decode_k<KV, D, 2>), g, dim3(1024), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4>), g, dim3(1024), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((attn_decode_k<KV, D, 1>), g, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((attn_decode_k<KV, D, 2>), g, dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4>), g, dim3(512), 0, s, a); break;
     default: return QT_ERR_SHAPE;
   }
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;

@@ -13,6 +13,7 @@
 //   epilogue (bias, SiLU/GELU, LayerScale, residual add, SwiGLU pairing) writes the output.
 // Decode (M <= 16) is HBM-bound on W: roofline = W bytes / 8 TB/s.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -26,6 +27,8 @@ struct GemmP {
   int act, epi;
   void* out; long long ldo;
   int taps, dil, cin, cin_pad, t_in, t_out, t_off;
+  int ks;                       // split-K factor (gridDim.y), 1 = none
+  unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
 };
 
 template <typename T> QT_DEV void load_vec(const T* p, float* o, int E);
@@ -183,15 +186,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   __shared__ float red_ss[WPB][16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lm = lane & 15, lk = lane >> 4;
-  const int nt = blockIdx.x;
+  const int nt = blockIdx.x, sp = blockIdx.y;
   const int ktiles = p.Kp / KT;
-  const int per = (ktiles + WPB - 1) / WPB;
-  const int kt0 = w * per, kt1 = min(ktiles, kt0 + per);
+  const int kps = (ktiles + p.ks - 1) / p.ks;  // k tiles of this split
+  const int ks0 = sp * kps, ks1 = min(ktiles, ks0 + kps);
+  const int per = (kps + WPB - 1) / WPB;
+  const int kt0 = ks0 + w * per, kt1 = min(ks1, kt0 + per);
   const bool rowok = lm < p.M;
   const int mrow = rowok ? lm : p.M - 1;
   const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[mrow] : (long long)mrow) * p.lda + lk * E;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f;
+  float ssv[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) ssv[i] = 0.f;
   // epilogue operands of wave 0 issued before the weight stream (hides one dependent round trip)
   const int n = nt * 16 + lm;
   const bool nval = n < p.N;
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 #pragma unroll
       for (int i = 0; i < E; ++i) {
         float x = ok ? a[u][i] : 0.f;
-        if constexpr (NORM) ss += x * x;
+        if constexpr (NORM) ssv[i] += x * x;  // E independent chains (not one 4*U*E-long chain)
         a[u][i] = x;
       }
       if constexpr (BF) {
@@ -238,27 +245,61 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   }
   red[w][lane][0] = acc[0]; red[w][lane][1] = acc[1]; red[w][lane][2] = acc[2]; red[w][lane][3] = acc[3];
   if (NORM) {
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) ss += ssv[i];
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
     if (lk == 0) red_ss[w][lm] = ss;
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  float v[4] = {0.f, 0.f, 0.f, 0.f}, ssr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ww = 0; ww < WPB; ++ww) {
     v[0] += red[ww][lane][0]; v[1] += red[ww][lane][1]; v[2] += red[ww][lane][2]; v[3] += red[ww][lane][3];
+  }
+  if (NORM) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ww = 0; ww < WPB; ++ww) ssr[i] += red_ss[ww][lk * 4 + i];
+  }
+  if (p.ks > 1) {
+    // deterministic split-K: every split stores its partial, the last to arrive sums them in split order.
+    // Agent-scope relaxed atomics (sc1: coherent across the 8 XCD L2s) + an explicit vmcnt drain instead of
+    // __threadfence(), whose release half is an XCD-wide L2 writeback (buffer_wbl2) costing ~0.4 us per block.
+    constexpr int PS = 64 * 4 + 16;
+    float* mine = p.part + ((size_t)nt * p.ks + sp) * PS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) __hip_atomic_store(mine + lane * 4 + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (NORM && lm == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(mine + 256 + lk * 4 + i, ssr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // partial stores acknowledged before the arrival is counted
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(p.cnt + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (old != (unsigned)p.ks - 1) return;
+    if (lane == 0) __hip_atomic_store(p.cnt + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    const float* base = p.part + (size_t)nt * p.ks * PS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = 0.f; ssr[i] = 0.f; }
+    for (int s = 0; s < p.ks; ++s) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] += __hip_atomic_load(base + s * PS + lane * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (NORM) ssr[i] += __hip_atomic_load(base + s * PS + 256 + lk * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   const float bias = pre_bias, cs = pre_cs;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float x = v[i];
-    if (NORM) {
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < WPB; ++ww) s += red_ss[ww][lk * 4 + i];
-      x *= rsqrtf(s / (float)p.Klog + p.eps);
-    }
+    if (NORM) x *= rsqrtf(ssr[i] / (float)p.Klog + p.eps);
     x += bias;
     if (p.act == QT_ACT_SILU) x = silu_f(x);
     else if (p.act == QT_ACT_GELU) x = gelu_f(x);
@@ -285,10 +326,17 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   }
 }
 
+template <typename WT, typename AT, typename OT, int WPB, int U>
+void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
+  if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
+  else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
+}
+
+// U = k tiles in flight per wave: 8 when a wave owns 5..8 (one round trip instead of two; measured slower at 12)
 template <typename WT, typename AT, typename OT, int WPB>
-void launch_gemv(const GemmP& p, int nt, hipStream_t s) {
-  if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, 4, true>), dim3(nt), dim3(WPB * 64), 0, s, p);
-  else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, 4, false>), dim3(nt), dim3(WPB * 64), 0, s, p);
+void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
+  if (per > 4 && per <= 8) launch_gemv_u<WT, AT, OT, WPB, 8>(p, nt, s);
+  else launch_gemv_u<WT, AT, OT, WPB, 4>(p, nt, s);
 }
 
 template <typename WT, typename AT, typename OT>
@@ -296,10 +344,10 @@ int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
   if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr) {
-    const int kts = p.Kp / KT;
-    if (kts >= 48) launch_gemv<WT, AT, OT, 16>(p, nt, s);
-    else if (kts >= 16) launch_gemv<WT, AT, OT, 8>(p, nt, s);
-    else launch_gemv<WT, AT, OT, 4>(p, nt, s);
+    const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
+    if (kts >= 48) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
+    else if (kts >= 16) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
+    else launch_gemv<WT, AT, OT, 4>(p, nt, (kts + 3) / 4, s);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
   } else if (p.M <= 32) {
@@ -347,6 +395,20 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.A = a->A; p.lda = a->lda; p.a_index = a->a_index; p.W = a->W;
   p.gamma = a->gamma; p.eps = a->eps; p.rms = a->rmsnorm || a->gamma != nullptr; p.bias = a->bias; p.colscale = a->colscale;
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
+  // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
+  p.ks = 1; p.cnt = nullptr; p.part = nullptr;
+  const int ntl = (a->N + 15) / 16, ktl = p.Kp / KT;
+  if (a->M <= 16 && a->taps == 0 && a->K % KT == 0 && a->gamma == nullptr && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN &&
+      a->splitk != 1 && ntl <= 4096) {
+    int ks = a->splitk > 1 ? a->splitk : (ntl >= 384 ? 1 : (512 + ntl - 1) / ntl);
+    ks = std::max(1, std::min({ks, 16, ktl / 2}));
+    const size_t need = 4096 * sizeof(unsigned) + (size_t)ntl * ks * (64 * 4 + 16) * sizeof(float);
+    if (ks > 1 && need <= (size_t)a->ws_bytes) {
+      p.ks = ks;
+      p.cnt = (unsigned*)a->ws;
+      p.part = (float*)((char*)a->ws + 4096 * sizeof(unsigned));
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;
   if (w == QT_BF16 && ad == QT_F32 && o == QT_F32) return launch<bf16_t, float, float>(p, s);

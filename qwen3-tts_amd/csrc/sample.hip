@@ -3,7 +3,7 @@
 // Greedy: argmax with lowest-index tie break (torch.argmax).
 // Sampling: Temperature -> TopK -> TopP -> softmax -> draw from a Philox-4x32-10 stream keyed by
 // (seed, step, substep, row).  Top-k threshold = exact k-th largest score, found by building its
-// order-preserving 32-bit key MSB-first (32 block-wide counts, no sort); ties at the threshold are kept
+// order-preserving 32-bit key MSB-first (<= 16 block-wide 2-bit steps, no sort); ties at the threshold are kept
 // like TopKLogitsWarper.  The draw is an inverse CDF over a fixed category order (parallel prefix of
 // per-thread masses), so it is an exact sample of the warped distribution; RNG streams differ from
 // torch.multinomial, hence parity is distribution-level (tests/test_gpu_parity.py).
@@ -58,7 +58,10 @@ QT_DEV float block_max(float v, float* sh) {
 __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
   __shared__ float sh[8];
   __shared__ int shi[4];
-  __shared__ int cntk[2][4];
+  __shared__ int cnt3[2][2][4];
+  __shared__ unsigned cand[256];
+  __shared__ int ncand;
+  __shared__ unsigned shtk;
   __shared__ float srt[4096];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = p.V;
@@ -110,15 +113,60 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
       unsigned key[PER];
 #pragma unroll
       for (int j = 0; j < PER; ++j) key[j] = (tid + j * NT < V) ? okey(s[j]) : 0u;
-      // MSB-first construction of the k-th largest key: one ballot count + one barrier per bit
-      for (int bit = 31; bit >= 0; --bit) {
-        const unsigned cand = tk | (1u << bit);
-        int c = 0;
+      // MSB-first construction of the k-th largest key, 2 bits per step.  Counts are per-thread VALU
+      // compares summed by packed wave reductions (n1 | n2 << 16, n3) and one barrier per step; the search
+      // stops as soon as exactly k keys are >= the prefix (that set is the top-k set).
+      int cur = V, bit = 30;
+      for (; bit >= 0 && cur != p.top_k && cur > 256; bit -= 2) {
+        const unsigned c1 = tk | (1u << bit), c2 = tk | (2u << bit), c3 = tk | (3u << bit);
+        int n12 = 0, n3 = 0;
 #pragma unroll
-        for (int j = 0; j < PER; ++j) c += __popcll(__ballot(key[j] >= cand));
-        if (lane == 0) cntk[bit & 1][w] = c;
+        for (int j = 0; j < PER; ++j) {
+          n12 += (key[j] >= c1 ? 1 : 0) + (key[j] >= c2 ? 0x10000 : 0);
+          n3 += key[j] >= c3 ? 1 : 0;
+        }
+        n12 = wave_sum_i(n12);
+        n3 = wave_sum_i(n3);
+        const int buf = (bit >> 1) & 1;
+        if (lane == 0) { cnt3[buf][0][w] = n12; cnt3[buf][1][w] = n3; }
         __syncthreads();
-        if (cntk[bit & 1][0] + cntk[bit & 1][1] + cntk[bit & 1][2] + cntk[bit & 1][3] >= p.top_k) tk = cand;
+        const int s12 = cnt3[buf][0][0] + cnt3[buf][0][1] + cnt3[buf][0][2] + cnt3[buf][0][3];
+        const int t3 = cnt3[buf][1][0] + cnt3[buf][1][1] + cnt3[buf][1][2] + cnt3[buf][1][3];
+        const int t1 = s12 & 0xFFFF, t2 = s12 >> 16;
+        if (t3 >= p.top_k) { tk = c3; cur = t3; }
+        else if (t2 >= p.top_k) { tk = c2; cur = t2; }
+        else if (t1 >= p.top_k) { tk = c1; cur = t1; }
+      }
+      if (bit >= 0 && cur != p.top_k) {
+        // <= 256 keys remain >= tk: compact them into LDS and finish the search in wave 0, barrier-free
+        if (tid == 0) ncand = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+          if (tid + j * NT < V && key[j] >= tk) cand[atomicAdd(&ncand, 1)] = key[j];
+        __syncthreads();
+        if (w == 0) {
+          unsigned ck[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ck[i] = lane + 64 * i < cur ? cand[lane + 64 * i] : 0u;
+          for (; bit >= 0 && cur != p.top_k; bit -= 2) {
+            const unsigned c1 = tk | (1u << bit), c2 = tk | (2u << bit), c3 = tk | (3u << bit);
+            int n12 = 0, n3 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              n12 += (ck[i] >= c1 ? 1 : 0) + (ck[i] >= c2 ? 0x10000 : 0);
+              n3 += ck[i] >= c3 ? 1 : 0;
+            }
+            const int s12 = wave_sum_i(n12), t3 = wave_sum_i(n3);
+            const int t1 = s12 & 0xFFFF, t2 = s12 >> 16;
+            if (t3 >= p.top_k) { tk = c3; cur = t3; }
+            else if (t2 >= p.top_k) { tk = c2; cur = t2; }
+            else if (t1 >= p.top_k) { tk = c1; cur = t1; }
+          }
+          if (lane == 0) shtk = tk;
+        }
+        __syncthreads();
+        tk = shtk;
       }
     }
     if (p.top_p < 1.0f) {  // rare path: sorted list (descending) for the nucleus cut

@@ -28,7 +28,10 @@ class GemmArgs(ctypes.Structure):
                 ("A", c_void_p), ("lda", c_ll), ("a_index", c_void_p), ("W", c_void_p), ("gamma", c_void_p),
                 ("eps", c_float), ("rmsnorm", c_int), ("bias", c_void_p), ("colscale", c_void_p), ("act", c_int), ("epi", c_int),
                 ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
-                ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int)]
+                ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int),
+                ("ws", c_void_p), ("ws_bytes", c_ll), ("splitk", c_int)]
+
+GEMM_WS_MIN = 4 << 20  # QT_GEMM_WS_MIN
 
 
 class QkvArgs(ctypes.Structure):

@@ -107,9 +107,22 @@ def tile_transconv(w, b, dtype, stride):
     return t
 
 
+_WS = {}
+
+
+def gemm_workspace(device):
+    """Split-K scratch of the decode GEMV for `device` (zeroed once; reused by every launch on the
+    process's single compute stream).  Allocate before any graph capture."""
+    idx = torch.device(device).index or 0
+    if idx not in _WS:
+        _WS[idx] = torch.zeros(_hip.GEMM_WS_MIN, dtype=torch.uint8, device=device)
+    return _WS[idx]
+
+
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
-         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True):
-    """conv = (t_in, t_out, t_off, dil) for implicit-conv weights."""
+         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0):
+    """conv = (t_in, t_out, t_off, dil) for implicit-conv weights.  splitk: 0 auto, 1 off, n forced
+    (decode GEMV only, needs gemm_workspace(device) allocated)."""
     a = _hip.GemmArgs()
     a.M, a.N, a.K = M, W.N, W.K
     a.a_dtype = _hip.dtype_code(a_dtype or A.dtype)
@@ -120,6 +133,9 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.bias = ptr(W.bias) if use_bias else None
     a.colscale, a.act, a.epi = ptr(colscale), act, epi
     a.out, a.ldo = ptr(out), ldo
+    ws = _WS.get(out.device.index or 0)
+    if ws is not None and M <= 16 and not W.taps:
+        a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
     if W.taps:
         t_in, t_out, t_off, dil = conv
         a.taps, a.dil, a.cin, a.cin_pad, a.t_in, a.t_out, a.t_off = W.taps, dil, W.cin, W.cin_pad, t_in, t_out, t_off

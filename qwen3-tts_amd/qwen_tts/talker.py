@@ -186,6 +186,7 @@ class TalkerEngine:
         s2m = "talker.code_predictor.small_to_mtp_projection.weight"
         self.s2m = K.tile_linear(_w(W, s2m, dev), wdt, _w(W, s2m.replace("weight", "bias"), dev)) if s2m in W else None
         self._sessions: Dict[tuple, Session] = {}
+        K.gemm_workspace(dev)  # split-K scratch of the decode GEMVs, allocated before any capture
         torch.cuda.synchronize()
 
     # ---------------------------------------------------------------- G1: prompt embeddings

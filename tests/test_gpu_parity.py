@@ -53,6 +53,41 @@ def test_gemm_linear(dtype, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(8, 1024, 3072), (3, 176, 1024), (16, 64, 512)])
+def test_gemv_splitk_deterministic(dtype, M, N, K):
+    """Decode GEMV split-K (last-arriving block reduces partials in split order): matches the unsplit
+    kernel to fp32 rounding, is bitwise reproducible, and keeps RMSNorm / bias / residual epilogues."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    Kn.gemm_workspace(dev)
+    g = torch.Generator().manual_seed(N + K)
+    W = torch.randn(N, K, generator=g) * 0.05
+    A = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).to(dev)
+    t = Kn.tile_linear(W.to(dev), dtype, b)
+    x0 = torch.randn(M, N, generator=g).to(dev)
+    outs = {}
+    for sk in (1, 2, 3, 4, 8, 0):
+        for rms in (False, True):
+            o = x0.clone()
+            Kn.gemm(A, t, o, M, K, N, rms=rms, eps=1e-6, epi=_hip.EPI_ADD, splitk=sk)
+            o2 = x0.clone()
+            Kn.gemm(A, t, o2, M, K, N, rms=rms, eps=1e-6, epi=_hip.EPI_ADD, splitk=sk)
+            assert torch.equal(o, o2), f"split-K {sk} not reproducible"
+            outs[(sk, rms)] = o.cpu()
+    Wr = W.to(dtype).float()
+    Aa = A.cpu().to(dtype).float() if dtype == torch.bfloat16 else A.cpu()
+    for rms in (False, True):
+        ref = Aa @ Wr.T
+        if rms:
+            ref = ref * torch.rsqrt(A.cpu().pow(2).mean(-1, keepdim=True) + 1e-6)
+        ref = x0.cpu() + ref + b.cpu()
+        for sk in (1, 2, 3, 4, 8, 0):
+            torch.testing.assert_close(outs[(sk, rms)], ref, atol=2e-4, rtol=2e-4)
+            torch.testing.assert_close(outs[(sk, rms)], outs[(1, rms)], atol=2e-5, rtol=2e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_swiglu_and_residual(dtype):
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
@@ -224,6 +259,52 @@ def test_sample_distribution_topk():
     p = torch.softmax(logits[0, V - 8:] / 0.9, -1)
     freq = torch.bincount(t - (V - 8), minlength=8).float() / R
     assert (freq - p).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("V,k,ties", [(3072, 50, False), (2048, 50, True), (3072, 300, False), (200, 7, True)])
+def test_sample_topk_support_large_vocab(V, k, ties):
+    """Exact k-th-largest threshold on realistic vocabularies (block search + LDS compaction + wave finish):
+    every draw lies in {scores >= k-th largest} (ties kept, TopKLogitsWarper), and the top token is drawn
+    at about its renormalised probability."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    R = 512
+    g = torch.Generator().manual_seed(V + k)
+    logits = torch.randn(R, V, generator=g) * 2
+    if ties:  # a block of equal scores straddling the threshold
+        kth = torch.topk(logits, k, -1).values[:, -1:]
+        idx = torch.randint(0, V, (R, 40), generator=g)
+        logits.scatter_(1, idx, kth.expand(R, 40))
+    thr = torch.topk(logits, k, -1).values[:, -1:]
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=k, top_p=1.0, temperature=1.0, seed=5,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    t = tok.cpu().long()
+    picked = logits.gather(1, t[:, None])
+    assert bool((picked >= thr).all())
+    # same row repeated: frequency of the argmax token vs its kept-set softmax probability
+    row = logits[:1].expand(4096, V).contiguous()
+    tok2 = torch.zeros(4096, dtype=torch.int32, device=dev)
+    Kn.sample(row.to(dev), 4096, V, V, tok2, do_sample=True, top_k=k, top_p=1.0, temperature=1.0, seed=9,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=1)
+    kept = torch.where(logits[0] >= thr[0], logits[0], torch.tensor(-float("inf")))
+    pr = torch.softmax(kept, -1)
+    top = int(torch.argmax(logits[0]))
+    assert abs((tok2.cpu().long() == top).float().mean().item() - pr[top].item()) < 0.03
+
+
+def test_sample_top_p_support():
+    """TopP keeps the smallest top set whose mass reaches top_p (TopPLogitsWarper semantics)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    V, R = 16, 1024
+    logits = torch.log(torch.tensor([0.4, 0.3, 0.15, 0.1] + [0.05 / 12] * 12))[None].expand(R, V).contiguous()
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=0, top_p=0.65, temperature=1.0, seed=3,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    t = tok.cpu().long()
+    assert set(t.tolist()) == {0, 1}  # 0.4 < 0.65 <= 0.4 + 0.3
+    assert abs((t == 0).float().mean().item() - 0.4 / 0.7) < 0.06
 
 
 # ------------------------------------------------------------------------------------------ end-to-end talker
