@@ -105,7 +105,7 @@ def kernel_roofline(tts, ids, languages, speakers, frames):
         from qwen_tts.talker import GenParams
         emb, mask, trail, pad = tts.model.build_prompts(ids, languages, speakers, None, False)
         gp = GenParams(max_new_tokens=frames + 1, ignore_eos=True)
-        eng.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=False, on_frames=on_frames)
+        eng.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=False, on_frames=on_frames, groups=1)
     finally:
         Kn.gemm = orig
     return rec.summary()
@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=24)
     ap.add_argument("--roofline", type=int, default=1)
+    ap.add_argument("--row-groups", type=int, default=1,
+                    help="decode the per-GPU batch as this many concurrent row groups (streams)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -167,6 +169,7 @@ def main():
                                         weights=W, codec_weights=CW)
     del W, CW
     torch.cuda.empty_cache()
+    tts.model.engine.row_groups = a.row_groups
     B = a.batch
     ids = [synth_ids(a.prompt_tokens, rank * 1000 + i) for i in range(B)]
     spk = (["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"] * 8)[:B]

@@ -118,7 +118,7 @@ typedef struct qt_decode_attn_args {
   const float* cos_tab; const float* sin_tab;
   const int* rope_pos; const int* row_batch; const int* kv_pos; const int* row_start;
   void* k_cache; void* v_cache; int kv_dtype;
-  float* out;
+  void* out; int o_dtype;  /* [R][Hq*D]; bf16 output = the rounding the next bf16 MFMA applies anyway */
 } qt_decode_attn_args;
 int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
 
@@ -141,6 +141,7 @@ typedef struct qt_sample_args {
   unsigned long long seed; const int* step; int substep;
   int* tok_out;
   int* codes; long long codes_ld; int codes_w; int codes_col; int codes_step_off;
+  int row_base;  /* global index of row 0: Philox stream id = row_base + r, so a batch split into row groups draws exactly the streams of the whole batch */
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 

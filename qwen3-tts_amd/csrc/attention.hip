@@ -360,7 +360,9 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
       ll += mrg_ml[ww][j][1] * f;
       oo += mrg_o[ww][j][d] * f;
     }
-    ((float*)p.out)[((long long)r * nq + h * NREP + j) * D + d] = oo / ll;
+    const long long oi = ((long long)r * nq + h * NREP + j) * D + d;
+    if (p.o_dtype == QT_BF16) ((bf16_t*)p.out)[oi] = f2bf(oo / ll);
+    else ((float*)p.out)[oi] = oo / ll;
   }
 }
 
@@ -404,6 +406,7 @@ extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool bf = a->kv_dtype == QT_BF16;
   if (!bf && a->kv_dtype != QT_F32) return QT_ERR_DTYPE;
+  if (a->o_dtype != QT_F32 && a->o_dtype != QT_BF16) return QT_ERR_DTYPE;
   switch (a->D) {
     case 16: return bf ? decode_dispatch<bf16_t, 16>(*a, s) : decode_dispatch<float, 16>(*a, s);
     case 64: return bf ? decode_dispatch<bf16_t, 64>(*a, s) : decode_dispatch<float, 64>(*a, s);

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
     for (int i = 0; i < w; ++i) off += sh[i];
     const float total = sh[0] + sh[1] + sh[2] + sh[3];
     inc += off;
-    const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)r) * total;
+    const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)(p.row_base + r)) * total;
     const float excl = inc - mass;
     if (tid == 0) shi[0] = -1;
     __syncthreads();

@@ -53,7 +53,7 @@ class DecodeAttnArgs(ctypes.Structure):
                 ("qkv", c_void_p), ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float),
                 ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("row_batch", c_void_p),
                 ("kv_pos", c_void_p), ("row_start", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
-                ("kv_dtype", c_int), ("out", c_void_p)]
+                ("kv_dtype", c_int), ("out", c_void_p), ("o_dtype", c_int)]
 
 
 class SampleArgs(ctypes.Structure):
@@ -63,7 +63,7 @@ class SampleArgs(ctypes.Structure):
                 ("finished", c_void_p), ("do_sample", c_int), ("top_k", c_int), ("top_p", c_float),
                 ("temperature", c_float), ("seed", c_ull), ("step", c_void_p), ("substep", c_int),
                 ("tok_out", c_void_p), ("codes", c_void_p), ("codes_ld", c_ll), ("codes_w", c_int),
-                ("codes_col", c_int), ("codes_step_off", c_int)]
+                ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int)]
 
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_sample", "qt_rmsnorm", "qt_gather_rows",

@@ -108,15 +108,34 @@ def tile_transconv(w, b, dtype, stride):
 
 
 _WS = {}
+_ACTIVE_WS = []
+
+
+def new_workspace(device):
+    """Split-K scratch of the decode GEMV (arrival counters must start at zero; every launch re-arms them).
+    One workspace per concurrently running stream."""
+    return torch.zeros(_hip.GEMM_WS_MIN, dtype=torch.uint8, device=device)
 
 
 def gemm_workspace(device):
-    """Split-K scratch of the decode GEMV for `device` (zeroed once; reused by every launch on the
-    process's single compute stream).  Allocate before any graph capture."""
+    """Default per-device workspace, for single-stream callers.  Allocate before any graph capture."""
     idx = torch.device(device).index or 0
     if idx not in _WS:
-        _WS[idx] = torch.zeros(_hip.GEMM_WS_MIN, dtype=torch.uint8, device=device)
+        _WS[idx] = new_workspace(device)
     return _WS[idx]
+
+
+class use_workspace:
+    """`with use_workspace(ws):` routes decode-GEMV split-K through `ws` (e.g. one per row-group stream)."""
+
+    def __init__(self, ws):
+        self.ws = ws
+
+    def __enter__(self):
+        _ACTIVE_WS.append(self.ws)
+
+    def __exit__(self, *exc):
+        _ACTIVE_WS.pop()
 
 
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
@@ -133,7 +152,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.bias = ptr(W.bias) if use_bias else None
     a.colscale, a.act, a.epi = ptr(colscale), act, epi
     a.out, a.ldo = ptr(out), ldo
-    ws = _WS.get(out.device.index or 0)
+    ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
     if ws is not None and M <= 16 and not W.taps:
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
     if W.taps:
@@ -170,13 +189,14 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
     a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
     a.rope_pos, a.row_batch, a.kv_pos, a.row_start = ptr(rope_pos), ptr(row_batch), ptr(kv_pos), ptr(row_start)
     a.k_cache, a.v_cache, a.kv_dtype, a.out = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype), ptr(out)
+    a.o_dtype = _hip.dtype_code(out.dtype)
     check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
 
 
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
-           codes_step_off=0):
+           codes_step_off=0, row_base=0):
     a = _hip.SampleArgs()
     a.logits, a.R, a.V, a.ld = ptr(logits), R, V, ld
     a.seen, a.rep_penalty = ptr(seen), rep_penalty
@@ -186,6 +206,7 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     a.do_sample, a.top_k, a.top_p, a.temperature = int(do_sample), int(top_k or 0), float(top_p), float(temperature)
     a.seed, a.step, a.substep, a.tok_out = seed & (2 ** 64 - 1), ptr(step), substep, ptr(tok_out)
     a.codes, a.codes_ld, a.codes_w, a.codes_col, a.codes_step_off = ptr(codes), codes_ld, codes_w, codes_col, codes_step_off
+    a.row_base = row_base
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 

@@ -10,6 +10,7 @@ Per-request state lives in a `Session` object, never on the module (fixes the re
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -56,6 +57,7 @@ class _Stack:
         self.theta = lc["rope_theta"]
         self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
         self.qkv_w = (self.Hq + 2 * self.Hkv) * self.D
+        self.wdt = wdt
 
     def ensure_rope(self, npos, dev):
         if self.cos.shape[0] < npos:
@@ -82,8 +84,12 @@ class _Stack:
 
 
 def _scratch(R, st: _Stack, dev):
+    """Per-forward activations.  The attention output and the SwiGLU output only feed the next GEMM's MFMA,
+    which rounds its A operand to the weight dtype anyway: in bf16 mode they are stored as bf16 (same RNE
+    rounding, half the bytes the o_proj / down GEMVs read)."""
     f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
-    return {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": f(R, st.Hq * st.D), "h": f(R, st.I)}
+    a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
+    return {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
 
 
 @dataclass
@@ -155,6 +161,8 @@ class Session:
         self.finished = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.trailing = f32(B, max_frames + 1, t.H)
         self.pad_embed = f32(t.H)
+        self.ws = K.new_workspace(dev)  # split-K scratch private to this session's stream
+        self.row_base = 0
         self.graph = None
 
 
@@ -186,7 +194,10 @@ class TalkerEngine:
         s2m = "talker.code_predictor.small_to_mtp_projection.weight"
         self.s2m = K.tile_linear(_w(W, s2m, dev), wdt, _w(W, s2m.replace("weight", "bias"), dev)) if s2m in W else None
         self._sessions: Dict[tuple, Session] = {}
-        K.gemm_workspace(dev)  # split-K scratch of the decode GEMVs, allocated before any capture
+        self._streams: List[torch.cuda.Stream] = []
+        # decode row groups: the batch is split into this many independent groups, each with its own session,
+        # HIP stream and captured frame graph; their latency-bound frames overlap on the GPU
+        self.row_groups = int(os.environ.get("QT_ROW_GROUPS", "1"))
         torch.cuda.synchronize()
 
     # ---------------------------------------------------------------- G1: prompt embeddings
@@ -217,15 +228,23 @@ class TalkerEngine:
         return out
 
     # ---------------------------------------------------------------- sessions / graph
-    def session(self, B, P, max_frames, gp: GenParams) -> Session:
+    def session(self, B, P, max_frames, gp: GenParams, row_base: int = 0) -> Session:
         P_cap = max(64, (P + 63) // 64 * 64)
-        key = (B, max_frames, gp.key())
+        key = (B, max_frames, gp.key(), row_base)
         s = self._sessions.get(key)
         if s is None or s.P_cap < P:
+            if any(k[1:3] != key[1:3] for k in self._sessions) or len(self._sessions) >= 8:
+                self._sessions.clear()  # keep only the live family of sessions (HBM)
             s = Session(self, B, P_cap, max_frames, gp)
+            s.row_base = row_base
             self.talker.ensure_rope(s.Lmax + 4, self.dev)
-            self._sessions = {key: s}  # keep one live session (HBM)
+            self._sessions[key] = s
         return s
+
+    def _stream(self, i):
+        while len(self._streams) <= i:
+            self._streams.append(torch.cuda.Stream(device=self.dev))
+        return self._streams[i]
 
     def _eos(self, gp):
         return gp.eos_token_id if gp.eos_token_id is not None else self.tc["codec_eos_token_id"]
@@ -238,7 +257,8 @@ class TalkerEngine:
                  suppress=(self.V - 1024, self.V, self.tc["codec_eos_token_id"]), ignore_eos=gp.ignore_eos,
                  finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
                  temperature=gp.temperature, seed=gp.seed, step=s.step, substep=substep, codes=s.codes,
-                 codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off)
+                 codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off,
+                 row_base=s.row_base)
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
@@ -278,16 +298,70 @@ class TalkerEngine:
         K.sample(s.cp_logits, s.B, self.Vc, self.Vc, s.cp_tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed=gp.seed, step=s.step, substep=1 + g, codes=s.codes, codes_ld=s.codes.shape[1] * self.G,
-                 codes_w=self.G, codes_col=1 + g, codes_step_off=0)
+                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
-                             tts_pad: torch.Tensor, gp: GenParams, use_graph: bool = True, on_frames=None):
-        """embeds fp32 [B,P,H] left-padded, mask [B,P] -> (codes list [F_i,16] int64 cpu, hidden list)."""
+                             tts_pad: torch.Tensor, gp: GenParams, use_graph: bool = True, on_frames=None,
+                             groups: Optional[int] = None):
+        """embeds fp32 [B,P,H] left-padded, mask [B,P] -> (codes list [F_i,16] int64 cpu, hidden list).
+
+        The batch is decoded as `groups` independent row groups (default self.row_groups), each on its own
+        HIP stream with its own session and captured frame graph; per-row arithmetic (and, through row_base,
+        each row's Philox stream) is the same as decoding the batch whole."""
+        B, P, H = embeds.shape
+        G = max(1, min(groups or self.row_groups, B))
+        max_frames = max(gp.max_new_tokens - 1, 0)
+        cuts = [B * i // G for i in range(G + 1)]
+        main = torch.cuda.current_stream(self.dev)
+        sessions, streams = [], []
+        for gi in range(G):
+            b0, b1 = cuts[gi], cuts[gi + 1]
+            st = self._stream(gi) if G > 1 else main
+            st.wait_stream(main)
+            s = self.session(b1 - b0, P, max(max_frames, 1), gp, row_base=b0)
+            with torch.cuda.stream(st), K.use_workspace(s.ws):
+                self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad)
+                if max_frames > 0 and use_graph and s.graph is None:
+                    s.graph = self._capture(s)
+            sessions.append(s)
+            streams.append(st)
+        frames = 0
+        check_every = 8
+        while frames < max_frames:
+            for s, st in zip(sessions, streams):
+                with torch.cuda.stream(st):
+                    s.hiddens[:, frames].copy_(s.past_hidden)
+                    if use_graph:
+                        s.graph.replay()
+                    else:
+                        with K.use_workspace(s.ws):
+                            self._frame(s)
+            frames += 1
+            if on_frames is not None:
+                on_frames(sessions[0], frames)
+            if frames % check_every == 0 or frames == max_frames:
+                if all(bool(s.finished.all()) for s in sessions):
+                    break
+        for st in streams:
+            main.wait_stream(st)
+        eos = self.tc["codec_eos_token_id"]
+        out_c, out_h = [], []
+        for s in sessions:
+            codes = s.codes[:, :frames].long().cpu()
+            hid = s.hiddens[:, :frames].cpu()
+            for b in range(s.B):
+                c0 = codes[b, :, 0]
+                stop = (c0 == eos).nonzero()
+                L = int(stop[0]) if stop.numel() else frames
+                out_c.append(codes[b, :L])
+                out_h.append(hid[b, :L])
+        return out_c, out_h
+
+    def _prefill(self, s: Session, embeds, mask, trailing, tts_pad):
+        """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s."""
         B, P, H = embeds.shape
         t = self.talker
-        max_frames = max(gp.max_new_tokens - 1, 0)
-        s = self.session(B, P, max(max_frames, 1), gp)
         dev = self.dev
         # reset per-request state
         for z in (s.seen, s.finished, s.codes, s.ctr):
@@ -325,34 +399,6 @@ class TalkerEngine:
         s.meta["kv_pos"].fill_(P)
         s.meta["row_len"].fill_(P + 1)
         s.meta["row_start"].copy_(n_pads.to(torch.int32))
-        frames = 0
-        if max_frames > 0:
-            if use_graph and s.graph is None:
-                s.graph = self._capture(s)
-            check_every = 8
-            while frames < max_frames:
-                s.hiddens[:, frames].copy_(s.past_hidden)
-                if use_graph:
-                    s.graph.replay()
-                else:
-                    self._frame(s)
-                frames += 1
-                if on_frames is not None:
-                    on_frames(s, frames)
-                if frames % check_every == 0 or frames == max_frames:
-                    if bool(s.finished.all()):
-                        break
-        codes = s.codes[:, :frames].long().cpu()
-        hid = s.hiddens[:, :frames].cpu()
-        eos = self.tc["codec_eos_token_id"]
-        out_c, out_h = [], []
-        for b in range(B):
-            c0 = codes[b, :, 0]
-            stop = (c0 == eos).nonzero()
-            L = int(stop[0]) if stop.numel() else frames
-            out_c.append(codes[b, :L])
-            out_h.append(hid[b, :L])
-        return out_c, out_h
 
     def _capture(self, s: Session):
         # the graph must not see the prefill-time counter values: it only reads device memory
@@ -360,7 +406,7 @@ class TalkerEngine:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), K.use_workspace(s.ws):
             with torch.cuda.graph(g, stream=side):
                 self._frame(s)
         torch.cuda.current_stream().wait_stream(side)

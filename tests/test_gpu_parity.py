@@ -219,6 +219,11 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
     torch.testing.assert_close(vc2.float(), vc.float(), atol=0, rtol=0)
     tol = 2e-5 if kvdt == torch.float32 else 2e-3
     torch.testing.assert_close(a2, a1, atol=tol, rtol=tol)
+    # bf16 output = RNE rounding of the fp32 output (what the o_proj MFMA would apply)
+    a3 = torch.zeros(B, hq * D, device=dev, dtype=torch.bfloat16)
+    kc3, vc3 = kc2.clone(), vc2.clone()
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, kvpos, start, kc3, vc3, L + 3, a3)
+    torch.testing.assert_close(a3, a2.to(torch.bfloat16), atol=0, rtol=0)
 
 
 def test_sample_greedy_processors():
@@ -361,6 +366,27 @@ def test_talker_eos_ragged_bit_exact(tiny_models):
     codes, _ = _run_case(model, key, dict(cases[key], max_new_tokens=24), list(cases).index(key), cfg)
     for j, c in enumerate(codes):
         np.testing.assert_array_equal(c.numpy(), z[f"eos_b2/codes{j}"])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_row_groups_identical_to_whole_batch(tiny_models, dtype):
+    """Decoding the batch as 2 or 3 concurrent row groups (own stream / session / graph each) reproduces the
+    whole-batch codes exactly, sampling included (Philox stream id = row_base + row)."""
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype=dtype)
+    case = dict(talker_cases()["cv_b3_auto_nospk"], do_sample=True, subtalker_dosample=True, seed=5)
+    ref = None
+    for groups in (1, 2, 3):
+        model.engine.row_groups = groups
+        codes, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
+        if ref is None:
+            ref = codes
+            continue
+        assert len(codes) == len(ref)
+        for a, b in zip(codes, ref):
+            np.testing.assert_array_equal(a.numpy(), b.numpy())
 
 
 def test_talker_bf16_runs_and_tracks_fp32(tiny_models):
