@@ -119,6 +119,8 @@ typedef struct qt_decode_attn_args {
   const int* rope_pos; const int* row_batch; const int* kv_pos; const int* row_start;
   void* k_cache; void* v_cache; int kv_dtype;
   void* out; int o_dtype;  /* [R][Hq*D]; bf16 output = the rounding the next bf16 MFMA applies anyway */
+  int const_pos;  /* >= 0: rope_pos = kv_pos = const_pos, row_start = 0, row_batch = r (code-predictor steps:
+                     static positions as a launch constant, so no dependent load precedes the K/V stream) */
 } qt_decode_attn_args;
 int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
 

@@ -207,12 +207,13 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int half = D / 2;
   const int nq = p.Hq, nk = p.Hkv;
-  const int b = p.row_batch[r];
-  const int kvpos = p.kv_pos[r];
+  const bool cpos = p.const_pos >= 0;
+  const int b = cpos ? r : p.row_batch[r];
+  const int kvpos = cpos ? p.const_pos : p.kv_pos[r];
   const long long base = ((long long)b * nk + h) * p.Lmax * D;
   const int grp = lane / LPK, sub = lane % LPK;
   const int gid = w * GPW + grp;
-  int start = p.row_start[r];
+  int start = cpos ? 0 : p.row_start[r];
   const int len = kvpos + 1;
   if (p.window > 0) start = max(start, len - p.window);
   const int n = len - start;  // keys [start, len); the last one (kvpos) comes from LDS
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
         const float rs = rsqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + p.eps);
         if (act) { x0 = nw[lane] * (x0 * rs); x1 = nw[lane + half] * (x1 * rs); }
       }
-      const int pos = p.rope_pos[r];
+      const int pos = cpos ? p.const_pos : p.rope_pos[r];
       if (act) {
         const float c = p.cos_tab[(long long)pos * half + lane], sn = p.sin_tab[(long long)pos * half + lane];
         const float y0 = x0 * c - x1 * sn, y1 = x1 * c + x0 * sn;

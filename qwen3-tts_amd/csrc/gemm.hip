@@ -14,6 +14,7 @@
 // Decode (M <= 16) is HBM-bound on W: roofline = W bytes / 8 TB/s.
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -28,6 +29,7 @@ struct GemmP {
   void* out; long long ldo;
   int taps, dil, cin, cin_pad, t_in, t_out, t_off;
   int ks;                       // split-K factor (gridDim.y), 1 = none
+  int wpb_max;                  // waves-per-block cap of the decode GEMV (16, or 8 for wide grids)
   unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
 };
 
@@ -345,8 +347,8 @@ int launch(const GemmP& p, hipStream_t s) {
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
   if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr) {
     const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
-    if (kts >= 48) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
-    else if (kts >= 16) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
+    if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
+    else if (kts >= 16 && p.wpb_max >= 8) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
     else launch_gemv<WT, AT, OT, 4>(p, nt, (kts + 3) / 4, s);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
@@ -397,6 +399,11 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
   // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
   p.ks = 1; p.cnt = nullptr; p.part = nullptr;
+  // wide grids use smaller blocks so several fit per CU (fewer block rounds; measured: N=12288 K=2048
+  // 14.7 us at 16 waves/block -> 12.0 at 4); QT_GEMV_WPB overrides the cap for A/B measurement
+  static const int wpb_env = [] { const char* e = getenv("QT_GEMV_WPB"); return e ? atoi(e) : 0; }();
+  const int ntc = (a->N + 15) / 16;
+  p.wpb_max = wpb_env > 0 ? wpb_env : (ntc > 512 ? 4 : (ntc > 256 ? 8 : 16));
   const int ntl = (a->N + 15) / 16, ktl = p.Kp / KT;
   if (a->M <= 16 && a->taps == 0 && a->K % KT == 0 && a->gamma == nullptr && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN &&
       a->splitk != 1 && ntl <= 4096) {

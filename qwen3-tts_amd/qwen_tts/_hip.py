@@ -53,7 +53,7 @@ class DecodeAttnArgs(ctypes.Structure):
                 ("qkv", c_void_p), ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float),
                 ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("row_batch", c_void_p),
                 ("kv_pos", c_void_p), ("row_start", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
-                ("kv_dtype", c_int), ("out", c_void_p), ("o_dtype", c_int)]
+                ("kv_dtype", c_int), ("out", c_void_p), ("o_dtype", c_int), ("const_pos", c_int)]
 
 
 class SampleArgs(ctypes.Structure):

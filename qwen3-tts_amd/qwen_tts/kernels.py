@@ -182,7 +182,7 @@ def attention(q, R, Hq, Hkv, D, kc, vc, Lmax, row_batch, row_start, row_len, out
 
 
 def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, row_start,
-                     kc, vc, Lmax, out, window=0):
+                     kc, vc, Lmax, out, window=0, const_pos=-1):
     a = _hip.DecodeAttnArgs()
     a.R, a.Hq, a.Hkv, a.D, a.Lmax, a.window = R, Hq, Hkv, D, Lmax, window
     a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
@@ -190,6 +190,7 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
     a.rope_pos, a.row_batch, a.kv_pos, a.row_start = ptr(rope_pos), ptr(row_batch), ptr(kv_pos), ptr(row_start)
     a.k_cache, a.v_cache, a.kv_dtype, a.out = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype), ptr(out)
     a.o_dtype = _hip.dtype_code(out.dtype)
+    a.const_pos = const_pos
     check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
 
 

@@ -72,7 +72,7 @@ class _Stack:
             if decode:
                 K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                    self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
-                                   meta["row_start"], kc, vc, Lmax, scratch["att"])
+                                   meta["row_start"], kc, vc, Lmax, scratch["att"], const_pos=meta.get("const_pos", -1))
             else:
                 K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
                            self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
@@ -144,7 +144,7 @@ class Session:
         for g in range(1, self.G - 1):
             pos = torch.full((B,), g + 1, dtype=torch.int32, device=dev)
             self.cp_meta.append({"rope_pos": pos, "kv_pos": pos.clone(), "row_len": pos + 1, "row_start": i32(B),
-                                 "row_batch": self.meta["row_batch"]})
+                                 "row_batch": self.meta["row_batch"], "const_pos": g + 1})
         f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.x = f32(B, t.H)
         self.past_hidden = f32(B, t.H)

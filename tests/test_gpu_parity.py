@@ -53,7 +53,7 @@ def test_gemm_linear(dtype, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(8, 1024, 3072), (3, 176, 1024), (16, 64, 512)])
+@pytest.mark.parametrize("M,N,K", [(8, 1024, 3072), (3, 176, 1024), (16, 64, 512), (8, 6144, 1024), (5, 4400, 2048)])
 def test_gemv_splitk_deterministic(dtype, M, N, K):
     """Decode GEMV split-K (last-arriving block reduces partials in split order): matches the unsplit
     kernel to fp32 rounding, is bitwise reproducible, and keeps RMSNorm / bias / residual epilogues."""
@@ -88,19 +88,21 @@ def test_gemv_splitk_deterministic(dtype, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_swiglu_and_residual(dtype):
+@pytest.mark.parametrize("H,I,sk", [(128, 192, 0), (256, 3072, 0), (256, 3072, 2)])
+def test_gemm_swiglu_and_residual(dtype, H, I, sk):
+    """SwiGLU epilogue (gate/up interleaved tiles, wide grid) + residual down-proj (auto / forced split-K)."""
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
     g = torch.Generator().manual_seed(3)
-    M, H, I = 8, 128, 192
+    M = 8
     gate, up, down = (torch.randn(I, H, generator=g) * 0.05, torch.randn(I, H, generator=g) * 0.05,
                       torch.randn(H, I, generator=g) * 0.05)
     x = torch.randn(M, H, generator=g)
     tgu, td = Kn.tile_swiglu(gate.to(dev), up.to(dev), dtype), Kn.tile_linear(down.to(dev), dtype)
     h = torch.zeros(M, I, device=dev)
-    Kn.gemm(x.to(dev), tgu, h, M, H, I, epi=_hip.EPI_SWIGLU)
+    Kn.gemm(x.to(dev), tgu, h, M, H, I, epi=_hip.EPI_SWIGLU, splitk=sk)
     xr = x.to(dev).clone()
-    Kn.gemm(h, td, xr, M, I, H, epi=_hip.EPI_ADD)
+    Kn.gemm(h, td, xr, M, I, H, epi=_hip.EPI_ADD, splitk=sk)
     c = lambda w: w.to(dtype).float()  # noqa: E731
     xa = x.to(dtype).float() if dtype == torch.bfloat16 else x
     hr = torch.nn.functional.silu(xa @ c(gate).T) * (xa @ c(up).T)
@@ -224,6 +226,15 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
     kc3, vc3 = kc2.clone(), vc2.clone()
     Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, kvpos, start, kc3, vc3, L + 3, a3)
     torch.testing.assert_close(a3, a2.to(torch.bfloat16), atol=0, rtol=0)
+    # static positions as a launch constant (code-predictor steps) == the same positions through device arrays
+    same, zero = i32([L - 1] * B), i32([0] * B)
+    kc4, vc4, kc5, vc5 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    a4 = torch.zeros(B, hq * D, device=dev)
+    a5 = torch.zeros(B, hq * D, device=dev)
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, same, rb, same, zero, kc4, vc4, L + 3, a4)
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, same, rb, same, zero, kc5, vc5, L + 3, a5,
+                        const_pos=L - 1)
+    assert torch.equal(a4, a5) and torch.equal(kc4, kc5) and torch.equal(vc4, vc5)
 
 
 def test_sample_greedy_processors():

@@ -38,7 +38,7 @@ ctr = torch.zeros(4, dtype=torch.int32, device=dev)
 timed(lambda: K.advance(ctr, 2), "advance (1 block, trivial)")
 K.gemm_workspace(dev)
 # cold weights: cycle through enough distinct matrices (> 256 MiB Infinity Cache) that every launch streams HBM;
-# split-K off (1) vs auto (0) vs forced factors, same box / same run
+# split-K off (1) vs auto (0) vs forced factors, same box / same run (QT_GEMV_WPB env caps waves per block)
 shapes = [(1024, 1024), (2048, 1024), (1024, 2048), (4096, 1024), (6144, 1024), (1024, 3072), (2048, 2048),
           (4096, 2048), (3072, 2048), (12288, 2048), (2048, 6144)]
 for (Nn, Kk) in shapes:
@@ -46,7 +46,7 @@ for (Nn, Kk) in shapes:
     Ws = [K.tile_linear(torch.randn(Nn, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
     A = torch.randn(8, Kk, device=dev)
     out = torch.zeros(8, Nn, device=dev)
-    for sk in (1, 0, 2, 4, 8):
+    for sk in (1, 0, 2, 4):  # 1 no split, 0 auto, n split-K
         for rms in ((False, True) if sk in (1, 0) else (False,)):
             it = {"i": 0}
 
