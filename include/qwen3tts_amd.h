@@ -64,6 +64,9 @@ typedef struct qt_gemm_args {
    * owned by the caller and used by one stream at a time; splitk 0 = auto, 1 = off, n = force n.
    * Partials are reduced in a fixed order by the last-arriving block: results are deterministic. */
   void* ws; long long ws_bytes; int splitk;
+  /* optional SnakeBeta on the A operand (K:577-615), per input channel: a' = a + inv_beta[c]*sin(alpha[c]*a)^2
+   * (alpha / inv_beta pre-exponentiated); fuses the activation that precedes every codec conv */
+  const float* snake_alpha; const float* snake_inv_beta;
 } qt_gemm_args;
 #define QT_GEMM_WS_MIN (4 << 20)
 

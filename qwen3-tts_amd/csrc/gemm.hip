@@ -30,8 +30,16 @@ struct GemmP {
   int taps, dil, cin, cin_pad, t_in, t_out, t_off;
   int ks;                       // split-K factor (gridDim.y), 1 = none
   int wpb_max;                  // waves-per-block cap of the decode GEMV (16, or 8 for wide grids)
+  int no_igemm;                 // 1: keep large-M GEMMs on gemm_wt (A/B measurement)
   unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
+  const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
 };
+
+// SnakeBeta exactly as qt_snake computes it (fp32 math on the stored activation)
+QT_DEV float snake1(float v, float al, float ib) {
+  const float s = sinf(v * al);
+  return v + ib * (s * s);
+}
 
 template <typename T> QT_DEV void load_vec(const T* p, float* o, int E);
 
@@ -56,6 +64,11 @@ QT_DEV void load_a(const GemmP& p, int m, int kk, float* v) {
     src = A + row * p.lda + kk;
   }
   if constexpr (E == 8) load8f(src, v); else load4f(src, v);
+  if (p.sn_a) {
+    const int c0 = p.taps > 0 ? (kk % p.cin_pad) : kk;
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = snake1(v[i], p.sn_a[c0 + i], p.sn_ib[c0 + i]);
+  }
 }
 
 template <typename WT, typename AT, typename OT, int MT, int WPB>
@@ -328,6 +341,169 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   }
 }
 
+// LDS-tiled implicit GEMM for large M with bf16 weights (codec convs / transposed convs as taps, prefill
+// linears as taps = 1).  Block = 128 output rows x 64 columns, 4 waves; wave w owns rows [32w, 32w+32) x all
+// 64 columns = 2 x 4 MFMA 16x16x32 tiles.  A tile's rows are one batch item's consecutive time steps, so the
+// input window [t0 + t_off, t0 + t_off + 127 + (taps-1)*dil] x 32 channels is staged into LDS once per channel
+// chunk (optional SnakeBeta applied while staging, rounded to bf16 like the MFMA operand) and every tap reads
+// its shifted rows from it: the im2col expansion (taps x) never leaves the CU.  The next chunk is loaded into
+// registers while the current one is multiplied (double-buffered window, one barrier per chunk).  Weights
+// are the pre-tiled MFMA B fragments (1 KiB per 16 x 32 tile), read through L1/L2 one tap ahead.
+// Row sums of squares (RMSNorm, taps == 1 only) accumulate from the fp32 A values during staging.
+constexpr int IG_BM = 128, IG_BN = 64, IG_KC = 32, IG_LDSW = 40;  // LDS row stride 40 bf16 (80 B)
+constexpr int IG_GPT = 3;  // staged 8-channel groups per thread (window rows <= 192)
+
+template <typename AT, typename OT>
+__global__ __launch_bounds__(256) void igemm_k(GemmP p) {
+  extern __shared__ unsigned char ig_smem[];
+  bf16_t* win = (bf16_t*)ig_smem;  // [2][WR][IG_LDSW]
+  __shared__ float ss_row[IG_BM];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lm = lane & 15, lk = lane >> 4;
+  const bool lin = p.taps == 0;
+  const int taps = lin ? 1 : p.taps, dil = lin ? 1 : p.dil;
+  const int cin = lin ? p.Klog : p.cin, cin_pad = lin ? p.Kp : p.cin_pad;
+  const int t_in = lin ? p.M : p.t_in, t_out = lin ? p.M : p.t_out, t_off = lin ? 0 : p.t_off;
+  const int WR = IG_BM + (taps - 1) * dil;
+  const int tiles_t = (t_out + IG_BM - 1) / IG_BM;
+  const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * IG_BM;
+  const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * 4;
+  const int nch = cin_pad / IG_KC, ktiles = p.Kp / IG_KC;
+  const AT* A = (const AT*)p.A + (long long)bi * t_in * p.lda;
+  const bool norm = p.rms != 0;
+
+  // staging: group q = tid + i*256 -> window row q/4, channels (q%4)*8 .. +8 of the chunk
+  float sst[IG_GPT];
+  float stg[IG_GPT][8];
+#pragma unroll
+  for (int i = 0; i < IG_GPT; ++i) sst[i] = 0.f;
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < IG_GPT; ++i) {
+      const int q = tid + i * 256, r = q >> 2, ch = c * IG_KC + (q & 3) * 8;
+      const int ti = t0 + t_off + r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) stg[i][e] = 0.f;
+      if (r < WR && ti >= 0 && ti < t_in && ch < cin) load8f(A + (long long)ti * p.lda + ch, stg[i]);
+    }
+  };
+  auto store_chunk = [&](int buf, int c) {
+    bf16_t* wb = win + (size_t)buf * WR * IG_LDSW;
+#pragma unroll
+    for (int i = 0; i < IG_GPT; ++i) {
+      const int q = tid + i * 256, r = q >> 2, ch = c * IG_KC + (q & 3) * 8;
+      if (r >= WR) continue;
+      float* v = stg[i];
+      if (p.sn_a && ch < cin) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = snake1(v[e], p.sn_a[ch + e], p.sn_ib[ch + e]);
+      }
+      if (norm) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sst[i] += v[e] * v[e];
+      }
+      *(u32x4_t*)(wb + r * IG_LDSW + (q & 3) * 8) =
+          u32x4_t{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+    }
+  };
+
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const bf16_t* Wb = (const bf16_t*)p.W + lane * 8;
+  auto load_b = [&](u32x4_t* bf, int kt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nt = min(nt0 + j, ntl - 1);
+      bf[j] = *(const u32x4_t*)(Wb + ((size_t)nt * ktiles + kt) * 512);
+    }
+  };
+
+  load_chunk(0);
+  store_chunk(0, 0);
+  __syncthreads();
+  u32x4_t bcur[4], bnxt[4];
+  load_b(bcur, 0);  // tap 0 of chunk 0 (k tile = tap * nch + chunk)
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) load_chunk(c + 1);
+    const bf16_t* wb = win + (size_t)buf * WR * IG_LDSW;
+    for (int j = 0; j < taps; ++j) {
+      // one tap ahead: next (tap, chunk) k tile
+      const int jn = j + 1 < taps ? j + 1 : 0, cn = j + 1 < taps ? c : c + 1;
+      if (cn < nch) load_b(bnxt, jn * nch + cn);
+      u32x4_t af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const u32x4_t*)(wb + (w * 32 + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                              __builtin_bit_cast(bf16x8_t, bcur[q]), acc[i][q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bcur[q] = bnxt[q];
+    }
+    if (c + 1 < nch) store_chunk(buf ^ 1, c + 1);
+    __syncthreads();
+  }
+  if (norm) {  // rows 0..127 staged by 4 consecutive lanes each (window == tile when taps == 1)
+#pragma unroll
+    for (int i = 0; i < IG_GPT; ++i) {
+      float s = sst[i];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      const int q = tid + i * 256, r = q >> 2;
+      if ((q & 3) == 0 && r < IG_BM) ss_row[r] = s;
+    }
+    __syncthreads();
+  }
+  OT* out = (OT*)p.out;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nt = nt0 + q;
+      if (nt >= ntl) continue;
+      const int n = nt * 16 + lm;
+      const bool nval = n < p.N;
+      const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
+      const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rl = w * 32 + i * 16 + lk * 4 + e;
+        float x = acc[i][q][e];
+        if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
+        x += bias;
+        if (p.act == QT_ACT_SILU) x = silu_f(x);
+        else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+        v[e] = x * cs;
+      }
+      if (p.epi == QT_EPI_SWIGLU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float up = __shfl_xor(v[e], 8, 64);
+          const int t = t0 + w * 32 + i * 16 + lk * 4 + e;
+          if (lm < 8 && t < t_out && nt * 8 + lm < (p.N >> 1))
+            out[((long long)bi * t_out + t) * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[e]) * up);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int t = t0 + w * 32 + i * 16 + lk * 4 + e;
+        if (t >= t_out || !nval) continue;
+        OT* o = out + ((long long)bi * t_out + t) * p.ldo + n;
+        if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[e]);
+        else *o = from_f<OT>(v[e]);
+      }
+    }
+  }
+}
+
 template <typename WT, typename AT, typename OT, int WPB, int U>
 void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
   if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
@@ -352,6 +528,14 @@ int launch(const GemmP& p, hipStream_t s) {
     else launch_gemv<WT, AT, OT, 4>(p, nt, (kts + 3) / 4, s);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
+  } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 && p.M >= 128 &&
+             (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
+    const int taps = p.taps == 0 ? 1 : p.taps, dil = p.taps == 0 ? 1 : p.dil;
+    const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;
+    const int WR = IG_BM + (taps - 1) * dil;
+    const size_t smem = (size_t)2 * WR * IG_LDSW * sizeof(bf16_t);
+    dim3 grid(batches * ((t_out + IG_BM - 1) / IG_BM), (nt + 3) / 4);
+    hipLaunchKernelGGL((igemm_k<AT, OT>), grid, dim3(256), smem, s, p);
   } else if (p.M <= 32) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 2, 8>), dim3(nt, (p.M + 31) / 32), dim3(512), 0, s, p);
   } else {
@@ -397,6 +581,10 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.A = a->A; p.lda = a->lda; p.a_index = a->a_index; p.W = a->W;
   p.gamma = a->gamma; p.eps = a->eps; p.rms = a->rmsnorm || a->gamma != nullptr; p.bias = a->bias; p.colscale = a->colscale;
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
+  p.sn_a = a->snake_alpha; p.sn_ib = a->snake_inv_beta;
+  if ((p.sn_a == nullptr) != (p.sn_ib == nullptr)) return QT_ERR_ARG;
+  static const int no_ig = [] { const char* e = getenv("QT_NO_IGEMM"); return e ? atoi(e) : 0; }();
+  p.no_igemm = no_ig;
   // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
   p.ks = 1; p.cnt = nullptr; p.part = nullptr;
   // wide grids use smaller blocks so several fit per CU (fewer block rounds; measured: N=12288 K=2048

@@ -29,7 +29,8 @@ class GemmArgs(ctypes.Structure):
                 ("eps", c_float), ("rmsnorm", c_int), ("bias", c_void_p), ("colscale", c_void_p), ("act", c_int), ("epi", c_int),
                 ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
                 ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int),
-                ("ws", c_void_p), ("ws_bytes", c_ll), ("splitk", c_int)]
+                ("ws", c_void_p), ("ws_bytes", c_ll), ("splitk", c_int),
+                ("snake_alpha", c_void_p), ("snake_inv_beta", c_void_p)]
 
 GEMM_WS_MIN = 4 << 20  # QT_GEMM_WS_MIN
 

@@ -107,12 +107,13 @@ class CodecDecoder:
         torch.cuda.synchronize()
 
     # ------------------------------------------------------------------------------------------------
-    def _conv(self, x, Wt, B, t_in, t_out, t_off, out, cin, epi=_hip.EPI_STORE, act=_hip.ACT_NONE):
-        K.gemm(x, Wt, out, B * t_out, cin, Wt.N, conv=(t_in, t_out, t_off, getattr(Wt, "dil", 1)), epi=epi, act=act)
+    def _conv(self, x, Wt, B, t_in, t_out, t_off, out, cin, epi=_hip.EPI_STORE, act=_hip.ACT_NONE, snake=None):
+        K.gemm(x, Wt, out, B * t_out, cin, Wt.N, conv=(t_in, t_out, t_off, getattr(Wt, "dil", 1)), epi=epi, act=act,
+               snake=snake)
 
-    def _causal(self, x, Wt, B, T, out, cin, epi=_hip.EPI_STORE):
+    def _causal(self, x, Wt, B, T, out, cin, epi=_hip.EPI_STORE, snake=None):
         dil = getattr(Wt, "dil", 1)
-        self._conv(x, Wt, B, T, T, -(Wt.taps - 1) * dil, out, cin, epi)
+        self._conv(x, Wt, B, T, T, -(Wt.taps - 1) * dil, out, cin, epi, snake=snake)
 
     def _transformer(self, h, B, T):
         """C3 (K:500-574).  h: [B*T][lat] (adt) -> [B*T][lat] (adt)."""
@@ -183,26 +184,20 @@ class CodecDecoder:
         self._causal(x, self.conv0, B, L, y, C)
         x, C = y, ds
         # C6
+        # every SnakeBeta feeds a conv: applied to the conv's A operand as it is staged (no separate pass)
         for blk in self.blocks:
             r, cout = blk["r"], blk["cout"]
-            tmp = torch.empty_like(x)
-            K.snake(x, tmp, B * L, C, *blk["s"])
             Lo = (L - 1) * r
             y = torch.empty(B * Lo, cout, dtype=adt, device=dev)
-            self._conv(tmp, blk["tconv"], B, L, L - 1, 0, y, C)
+            self._conv(x, blk["tconv"], B, L, L - 1, 0, y, C, snake=blk["s"])
             L, C, x = Lo, cout, y
-            a = torch.empty_like(x)
             bb = torch.empty_like(x)
             for un in blk["units"]:
-                K.snake(x, a, B * L, C, *un["s1"])
-                self._causal(a, un["c1"], B, L, bb, C)
-                K.snake(bb, a, B * L, C, *un["s2"])
-                self._causal(a, un["c2"], B, L, x, C, epi=_hip.EPI_ADD)
+                self._causal(x, un["c1"], B, L, bb, C, snake=un["s1"])
+                self._causal(bb, un["c2"], B, L, x, C, epi=_hip.EPI_ADD, snake=un["s2"])
         # C7
-        tmp = torch.empty_like(x)
-        K.snake(x, tmp, B * L, C, *self.s_last)
         out = torch.empty(B * L, self.conv_last.N, dtype=torch.float32, device=dev)
-        self._conv(tmp, self.conv_last, B, L, L, -(self.conv_last.taps - 1), out, C)
+        self._conv(x, self.conv_last, B, L, L, -(self.conv_last.taps - 1), out, C, snake=self.s_last)
         pcm = out[:, 0].contiguous()
         K.clamp_pcm(pcm, pcm.numel(), pcm)
         return pcm.view(B, L)

@@ -139,9 +139,10 @@ class use_workspace:
 
 
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
-         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0):
+         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0, snake=None):
     """conv = (t_in, t_out, t_off, dil) for implicit-conv weights.  splitk: 0 auto, 1 off, n forced
-    (decode GEMV only, needs gemm_workspace(device) allocated)."""
+    (decode GEMV only, needs gemm_workspace(device) allocated).  snake = (alpha, inv_beta): SnakeBeta applied
+    to A per input channel inside the GEMM (fused codec activation)."""
     a = _hip.GemmArgs()
     a.M, a.N, a.K = M, W.N, W.K
     a.a_dtype = _hip.dtype_code(a_dtype or A.dtype)
@@ -152,6 +153,8 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.bias = ptr(W.bias) if use_bias else None
     a.colscale, a.act, a.epi = ptr(colscale), act, epi
     a.out, a.ldo = ptr(out), ldo
+    if snake is not None:
+        a.snake_alpha, a.snake_inv_beta = ptr(snake[0]), ptr(snake[1])
     ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
     if ws is not None and M <= 16 and not W.taps:
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk

@@ -148,6 +148,82 @@ def test_gemm_transposed_conv(cin, cout, s):
         torch.testing.assert_close(out.view(B, tout * s, cout).permute(0, 2, 1).cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _snake_ref(x, al, ib):  # channels on dim 1 (NCT), same fp32 formula as the kernels
+    return x + ib[None, :, None] * torch.sin(x * al[None, :, None]) ** 2
+
+
+@pytest.mark.parametrize("cin,cout,k,dil,T", [(64, 96, 7, 9, 300), (96, 64, 7, 1, 129), (32, 48, 1, 1, 257),
+                                             (64, 768, 7, 3, 140), (160, 32, 7, 9, 64)])
+@pytest.mark.parametrize("snake", [False, True])
+def test_igemm_conv_bf16(cin, cout, k, dil, T, snake):
+    """LDS-tiled implicit-GEMM conv (bf16 weights/activations, several 128-row tiles per batch item, ragged
+    tail, window up to 182 rows) with optional fused SnakeBeta, against torch conv1d on the same roundings."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(cin * 7 + cout + k + dil)
+    B = 3
+    w, b = torch.randn(cout, cin, k, generator=g) * 0.05, torch.randn(cout, generator=g) * 0.1
+    x = _bf(torch.randn(B, cin, T, generator=g))
+    al, ib = torch.exp(0.3 * torch.randn(cin, generator=g)), torch.exp(-0.3 * torch.randn(cin, generator=g))
+    xin = _bf(_snake_ref(x, al, ib)) if snake else x
+    ref = torch.nn.functional.conv1d(torch.nn.functional.pad(xin, ((k - 1) * dil, 0)), _bf(w), b, dilation=dil)
+    res = torch.randn(B, cout, T, generator=g)
+    t = Kn.tile_conv(w.to(dev), b.to(dev), torch.bfloat16, dil)
+    xl = x.permute(0, 2, 1).contiguous().to(dev, torch.bfloat16)
+    out = res.permute(0, 2, 1).contiguous().reshape(B * T, cout).to(dev)
+    Kn.gemm(xl, t, out, B * T, cin, cout, conv=(T, T, -(k - 1) * dil, dil), epi=_hip.EPI_ADD,
+            snake=(al.to(dev), ib.to(dev)) if snake else None)
+    got = out.view(B, T, cout).permute(0, 2, 1).cpu()
+    torch.testing.assert_close(got, ref + res, atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("s", [2, 5, 8])
+def test_igemm_transposed_conv_bf16(s):
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(s + 100)
+    B, T, cin, cout = 2, 150, 64, 48
+    x = _bf(torch.randn(B, cin, T, generator=g))
+    w, b = torch.randn(cin, cout, 2 * s, generator=g) * 0.05, torch.randn(cout, generator=g) * 0.1
+    y = torch.nn.functional.conv_transpose1d(x, _bf(w), b, stride=s)
+    ref = y[..., s:y.shape[-1] - s]
+    t = Kn.tile_transconv(w.to(dev), b.to(dev), torch.bfloat16, s)
+    out = torch.zeros(B * (T - 1) * s, cout, device=dev)
+    Kn.gemm(x.permute(0, 2, 1).contiguous().to(dev, torch.bfloat16), t, out, B * (T - 1), cin, s * cout,
+            conv=(T, T - 1, 0, 1))
+    torch.testing.assert_close(out.view(B, (T - 1) * s, cout).permute(0, 2, 1).cpu(), ref, atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M", [128, 300])
+def test_igemm_linear_rms_swiglu_bf16(M):
+    """Large-M linears on the tiled path: folded-gamma RMSNorm rows, SwiGLU epilogue, residual add."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(M)
+    H, I = 256, 384
+    x = torch.randn(M, H, generator=g)
+    gamma = 1 + 0.1 * torch.randn(H, generator=g)
+    gate, up = torch.randn(I, H, generator=g) * 0.05, torch.randn(I, H, generator=g) * 0.05
+    tgu = Kn.tile_swiglu(gate.to(dev), up.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+    h = torch.zeros(M, I, device=dev)
+    Kn.gemm(x.to(dev), tgu, h, M, H, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU)
+    rs = torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-6)
+    xa = _bf(x)
+    hg = (xa @ _bf(gate * gamma).T) * rs
+    hu = (xa @ _bf(up * gamma).T) * rs
+    torch.testing.assert_close(h.cpu(), torch.nn.functional.silu(hg) * hu, atol=2e-3, rtol=2e-3)
+    down = torch.randn(H, I, generator=g) * 0.05
+    td = Kn.tile_linear(down.to(dev), torch.bfloat16)
+    hb = h.to(torch.bfloat16)
+    xr = x.to(dev).clone()
+    Kn.gemm(hb, td, xr, M, I, H, epi=_hip.EPI_ADD)
+    torch.testing.assert_close(xr.cpu(), x + _bf(hb.cpu().float()) @ _bf(down).T, atol=2e-3, rtol=2e-3)
+
+
 @pytest.mark.parametrize("D,hq,hkv,window", [(128, 16, 8, 0), (16, 4, 2, 0), (64, 4, 4, 5)])
 def test_qkv_post_and_attention(D, hq, hkv, window):
     from qwen_tts import kernels as Kn
