@@ -504,6 +504,59 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   }
 }
 
+// Single-output-channel causal conv (codec conv_last, Cout = 1): memory-bound, so no MFMA.  A block owns
+// 256 consecutive outputs of one batch item; the input window (256 + (taps-1)*dil rows) x 32 channels is staged
+// in LDS per channel chunk (SnakeBeta applied on staging) and each thread accumulates its output's taps x cin
+// products in fp32.  Weights are read from the row-major [taps][cin_pad] tile row 0 (N = 1 -> tile 0, lane
+// group layout: element (k) of tile kt sits at lane (k % 32) / 8 * 16, offset k % 8).
+template <typename AT, typename WT, typename OT>
+__global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
+  constexpr int KC = 32, WS = KC + 1;
+  extern __shared__ float c1_win[];  // [WR][WS]
+  const int tid = threadIdx.x;
+  const int taps = p.taps, dil = p.dil;
+  const int WR = 256 + (taps - 1) * dil;
+  const int tiles_t = (p.t_out + 255) / 256;
+  const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * 256;
+  const AT* A = (const AT*)p.A + (long long)bi * p.t_in * p.lda;
+  const WT* W = (const WT*)p.W;
+  constexpr int E = sizeof(WT) == 2 ? 8 : 4, KT = 4 * E;
+  __shared__ float wsh[2048];  // taps * cin_pad weights of output channel 0 (host checks the size)
+  for (int k = tid; k < taps * p.cin_pad; k += 256) {
+    const int kt = k / KT, kin = k % KT;
+    wsh[k] = to_f(W[(size_t)kt * 64 * E + (kin / E) * 16 * E + (kin % E)]);
+  }
+  float acc = 0.f;
+  for (int c0 = 0; c0 < p.cin; c0 += KC) {
+    __syncthreads();
+    for (int q = tid; q < WR * KC; q += 256) {
+      const int r = q / KC, c = c0 + q % KC;
+      const int ti = t0 + p.t_off + r;
+      float v = 0.f;
+      if (ti >= 0 && ti < p.t_in && c < p.cin) {
+        v = to_f(A[(long long)ti * p.lda + c]);
+        if (p.sn_a) v = snake1(v, p.sn_a[c], p.sn_ib[c]);
+        if (sizeof(WT) == 2) v = __uint_as_float((unsigned)f2bf(v) << 16);  // bf16 operand, as the MFMA paths
+      }
+      c1_win[r * WS + q % KC] = v;
+    }
+    __syncthreads();
+    for (int j = 0; j < taps; ++j) {
+      const float* row = c1_win + (tid + j * dil) * WS;
+      const float* wr = wsh + j * p.cin_pad + c0;  // K index of the [1][taps*cin_pad] weight row
+      const int nc = min(KC, p.cin - c0);
+#pragma unroll 8
+      for (int cc = 0; cc < nc; ++cc) acc += wr[cc] * row[cc];
+    }
+  }
+  const int t = t0 + tid;
+  if (t < p.t_out) {
+    float x = acc + (p.bias ? p.bias[0] : 0.f);
+    OT* o = (OT*)p.out + ((long long)bi * p.t_out + t) * p.ldo;
+    *o = from_f<OT>(p.epi == QT_EPI_ADD ? to_f(*o) + x : x);
+  }
+}
+
 template <typename WT, typename AT, typename OT, int WPB, int U>
 void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
   if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
@@ -526,6 +579,13 @@ int launch(const GemmP& p, hipStream_t s) {
     if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
     else if (kts >= 16 && p.wpb_max >= 8) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
     else launch_gemv<WT, AT, OT, 4>(p, nt, (kts + 3) / 4, s);
+  } else if (p.N == 1 && p.taps > 0 && p.taps * p.cin_pad <= 2048 && p.act == QT_ACT_NONE &&
+             p.epi != QT_EPI_SWIGLU && !p.rms &&
+             p.colscale == nullptr && p.a_index == nullptr && p.gamma == nullptr &&
+             (size_t)(256 + (p.taps - 1) * p.dil) * 33 * sizeof(float) <= 64 * 1024) {
+    const size_t smem = (size_t)(256 + (p.taps - 1) * p.dil) * 33 * sizeof(float);
+    const int batches = p.M / p.t_out;
+    hipLaunchKernelGGL((conv_n1_k<AT, WT, OT>), dim3(batches * ((p.t_out + 255) / 256)), dim3(256), smem, s, p);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
   } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 && p.M >= 128 &&
