@@ -52,63 +52,48 @@ def make_weights(preset, dev, world, rank):
     return cfg, W, CW
 
 
-class GemmRecorder:
-    """Times every qt_gemm launch of one eager frame with HIP events (same stream) and sums the
-    algorithmic bytes each launch must move: weights + activations in + activations out."""
-
-    def __init__(self):
-        self.recs = []
-
-    def __call__(self, fn, A, W, out, M, *a, **k):
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        fn(A, W, out, M, *a, **k)
-        ev1.record()
-        wbytes = W.w.numel() * W.w.element_size()
-        abytes = M * W.K * (A.element_size() if k.get("a_dtype") is None else 2)
-        obytes = M * W.N * out.element_size() * (2 if k.get("epi") == 1 else 1)
-        self.recs.append((ev0, ev1, wbytes + abytes + obytes, M))
-
-    def summary(self):
-        torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b, _, _ in self.recs]
-        by = [r[2] for r in self.recs]
-        n = len(ms)
-        tot_ms, tot_b = sum(ms), sum(by)
-        return dict(launches=n, avg_us=1e3 * tot_ms / n, bytes_per_launch=tot_b / n, gbs=tot_b / (tot_ms * 1e-3) / 1e9)
+ROOF_KERNEL = "gemv_wt<bf16,f32,bf16,WPB=4,U=4,rms> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
 
 
-def kernel_roofline(tts, ids, languages, speakers, frames):
-    """One extra eager (non-graph) generate of a few frames with per-launch HIP events on qt_gemm."""
-    from qwen_tts import kernels as Kn
-    rec = GemmRecorder()
-    orig = Kn.gemm
-    started = {"on": False}
+def gateup_bytes(eng, B):
+    """Algorithmic HBM bytes of one talker gate-up launch: bf16 weight tiles + fp32 A rows + bf16 SwiGLU out."""
+    t = eng.talker
+    L = t.layers[0].gu
+    return L.w.numel() * L.w.element_size() + B * t.H * 4 + B * t.I * 2
 
-    def hooked(A, W, out, M, *a, **k):
-        if started["on"]:
-            rec(orig, A, W, out, M, *a, **k)
-        else:
-            orig(A, W, out, M, *a, **k)
 
+def kernel_roofline(tts, B, reps=10):
+    """Dominant decode kernel timed live: a HIP graph of the 28 production gate-up launches (one per layer,
+    distinct weights, so every launch streams HBM as in a frame), replayed `reps` times between HIP events
+    recorded on the capture stream.  Per-launch time includes the in-graph dispatch gap (conservative)."""
+    from qwen_tts import _hip, kernels as Kn
     eng = tts.model.engine
+    t = eng.talker
+    dev = eng.dev
+    x = torch.randn(B, t.H, device=dev)
+    h = torch.empty(B, t.I, dtype=eng.wdt, device=dev)
 
-    def on_frames(s, n):
-        # skip the prefill; before the recorded frames are enqueued, park the GPU on a spin kernel so the
-        # host (ctypes launches) runs ahead and the events time back-to-back kernels, not enqueue gaps
-        if n == 1:
-            torch.cuda._sleep(int(3e8))
-        started["on"] = n >= 1
-
-    Kn.gemm = hooked
-    try:
-        from qwen_tts.talker import GenParams
-        emb, mask, trail, pad = tts.model.build_prompts(ids, languages, speakers, None, False)
-        gp = GenParams(max_new_tokens=frames + 1, ignore_eos=True)
-        eng.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=False, on_frames=on_frames, groups=1)
-    finally:
-        Kn.gemm = orig
-    return rec.summary()
+    def run():
+        for L in t.layers:
+            Kn.gemm(x, L.gu, h, B, t.H, t.I, rms=True, eps=t.eps, epi=_hip.EPI_SWIGLU)
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        run()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            run()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            g.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    n = reps * len(t.layers)
+    us = e0.elapsed_time(e1) * 1e3 / n
+    byt = gateup_bytes(eng, B)
+    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, launches=n)
 
 
 def cpu_baseline(B, prompt, frames, threads):
@@ -208,16 +193,15 @@ def main():
     value = audio / dt
     roof = None
     if a.roofline and rank == 0:
-        r = kernel_roofline(tts, ids, langs, spk, 4)
+        r = kernel_roofline(tts, B)
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_gemm_decode.json")
+        pmc = os.path.join(REPO, "profiles", "r01_pmc_gateup.json")
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        roof = {"bound": "hbm", "kernel": "gemm_wt<bf16,f32,f32,1,8> (decode weight-streaming GEMV)",
-                "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes_per_launch"]),
-                "launches_per_frame": r["launches"] // 3}
+        roof = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),
+                "timed_launches": r["launches"]}
     cpu = None
     if a.cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, int(os.environ.get("OMP_NUM_THREADS", "16")))
