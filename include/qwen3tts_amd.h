@@ -128,6 +128,26 @@ typedef struct qt_decode_attn_args {
 int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * qt_mlp_decode: one decode step of the Qwen3 MLP with its residual, fused (M:655-668: down_proj(act(gate_proj
+ * (x)) * up_proj(x)) after the post-attention RMSNorm, + residual): x[m] += W_down(silu(W_gate n(x)) * W_up n(x)).
+ * M <= 16 rows (fp32 residual x, row stride ldx), H in {1024, 2048}, I % 32 == 0, H/16 <= I/32 <= 256;
+ * bf16 weight tiles from qt_tile_weight: w_gu = gate/up interleaved 8+8 rows per tile with the RMSNorm gamma
+ * folded in, w_down = [H][I].  ws: zero-initialised device scratch of >= qt_mlp_ws_bytes(M, H, I), used by
+ * one stream at a time; err (optional device int) is set to 1 if the in-kernel arrival wait timed out.
+ * Deterministic: partials are reduced in block order.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_mlp_args {
+  int M, H, I;
+  float* x; long long ldx;
+  const void* w_gu; const void* w_down;
+  float eps;
+  void* ws; long long ws_bytes;
+  int* err;
+} qt_mlp_args;
+long long qt_mlp_ws_bytes(int M, int H, int I);
+int qt_mlp_decode(const qt_mlp_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * qt_sample: transformers-4.57 logits processing + token choice, one row per block.
  * RepetitionPenalty (seen flags) -> MinNewTokens (mask eos while *n_generated < min_new_tokens) ->
  * SuppressTokens [suppress_lo, suppress_hi) except suppress_keep (+ eos when ignore_eos) ->

@@ -67,8 +67,14 @@ class SampleArgs(ctypes.Structure):
                 ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int)]
 
 
-EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_sample", "qt_rmsnorm", "qt_gather_rows",
-           "qt_frame_embed", "qt_advance", "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
+class MlpArgs(ctypes.Structure):
+    _fields_ = [("M", c_int), ("H", c_int), ("I", c_int), ("x", c_void_p), ("ldx", c_ll), ("w_gu", c_void_p),
+                ("w_down", c_void_p), ("eps", c_float), ("ws", c_void_p), ("ws_bytes", c_ll), ("err", c_void_p)]
+
+
+EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_mlp_ws_bytes",
+           "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
+           "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
 
 _LIB = None
 
@@ -90,12 +96,12 @@ def load_library(path: str = LIB_PATH):
         "qt_rvq_gather": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P],
         "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
-        "qt_clamp_pcm": [P, c_int, c_ll, P, P],
+        "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
     }
     for name, args in sig.items():
         f = getattr(L, name)
         f.argtypes = args
-        f.restype = c_int
+        f.restype = c_ll if name == "qt_mlp_ws_bytes" else c_int
     return L
 
 

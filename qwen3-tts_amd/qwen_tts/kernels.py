@@ -164,6 +164,23 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     check(_hip.lib().qt_gemm(ctypes.byref(a), stream()), "qt_gemm")
 
 
+def mlp_ws_bytes(M, H, I):
+    return int(_hip.lib().qt_mlp_ws_bytes(M, H, I))
+
+
+def mlp_supported(H, I, wdt) -> bool:
+    return wdt == torch.bfloat16 and H in (1024, 2048) and I % 32 == 0 and H // 16 <= I // 32 <= 256
+
+
+def mlp_decode(x, M, H, I, w_gu: "Tiled", w_down: "Tiled", eps, ws, err=None):
+    """Fused decode MLP + residual (qt_mlp_decode): x[:M] += down(SwiGLU(rms(x) gate/up)); x fp32 [M][H]."""
+    a = _hip.MlpArgs()
+    a.M, a.H, a.I, a.x, a.ldx = M, H, I, ptr(x), x.stride(0)
+    a.w_gu, a.w_down, a.eps = ptr(w_gu.w), ptr(w_down.w), eps
+    a.ws, a.ws_bytes, a.err = ptr(ws), ws.numel() * ws.element_size(), ptr(err)
+    check(_hip.lib().qt_mlp_decode(ctypes.byref(a), stream()), "qt_mlp_decode")
+
+
 def qkv_post(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, q_out, kc, vc, Lmax):
     a = _hip.QkvArgs()
     a.R, a.Hq, a.Hkv, a.D = R, Hq, Hkv, D

@@ -79,8 +79,17 @@ class _Stack:
                 K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
-            K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
-            K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
+            if "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
+                K.mlp_decode(x, R, self.H, self.I, L.gu, L.down, self.eps, scratch["mlp_ws"], scratch["mlp_err"])
+            else:
+                K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
+                K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
+
+
+# qt_mlp_decode (one-launch MLP) is correct and tested but measured slower than the two GEMVs on MI355X
+# (CP 17.1 vs 14.6 us, talker 31.6 vs 22.8 us: its 96-192 blocks stream the weights through fewer CUs and the
+# cross-block reduction adds ~3 dependent round trips), so it is opt-in.
+FUSED_MLP = os.environ.get("QT_FUSED_MLP", "0") == "1"
 
 
 def _scratch(R, st: _Stack, dev):
@@ -89,7 +98,11 @@ def _scratch(R, st: _Stack, dev):
     rounding, half the bytes the o_proj / down GEMVs read)."""
     f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
     a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
-    return {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
+    sc = {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
+    if FUSED_MLP and R <= 16 and K.mlp_supported(st.H, st.I, st.wdt):  # fused decode MLP scratch
+        sc["mlp_ws"] = torch.zeros(K.mlp_ws_bytes(R, st.H, st.I), dtype=torch.uint8, device=dev)
+        sc["mlp_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return sc
 
 
 @dataclass
@@ -345,6 +358,10 @@ class TalkerEngine:
                     break
         for st in streams:
             main.wait_stream(st)
+        for s in sessions:
+            for sc in (s.sc_t, s.sc_c):
+                if "mlp_err" in sc and int(sc["mlp_err"].item()):
+                    raise RuntimeError("qt_mlp_decode: in-kernel arrival wait timed out (results invalid)")
         eos = self.tc["codec_eos_token_id"]
         out_c, out_h = [], []
         for s in sessions:

@@ -9,7 +9,7 @@ def test_library_exports_every_declared_symbol():
     from qwen_tts import _hip
     L = _hip.load_library()
     hdr = open(os.path.join(REPO, "include", "qwen3tts_amd.h")).read()
-    declared = set(re.findall(r"\bint (qt_\w+)\(", hdr))
+    declared = set(re.findall(r"\b(?:int|long long) (qt_\w+)\(", hdr))
     assert declared == set(_hip.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name

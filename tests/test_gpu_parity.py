@@ -148,6 +148,37 @@ def test_gemm_transposed_conv(cin, cout, s):
         torch.testing.assert_close(out.view(B, tout * s, cout).permute(0, 2, 1).cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M,H,I", [(8, 1024, 3072), (16, 1024, 3072), (3, 1024, 2048), (8, 2048, 6144)])
+def test_mlp_decode_fused(M, H, I):
+    """Fused decode MLP (one launch, deterministic cross-block reduction) == the two-GEMV path
+    (gate/up + SwiGLU to bf16, down + residual) to fp32 summation order; bit-reproducible across launches
+    (counters re-armed), no arrival timeout."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(M + H + I)
+    gamma = 1 + 0.1 * torch.randn(H, generator=g)
+    gate, up = torch.randn(I, H, generator=g) * 0.03, torch.randn(I, H, generator=g) * 0.03
+    down = torch.randn(H, I, generator=g) * 0.03
+    tgu = Kn.tile_swiglu(gate.to(dev), up.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+    td = Kn.tile_linear(down.to(dev), torch.bfloat16)
+    ws = torch.zeros(Kn.mlp_ws_bytes(M, H, I), dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    for it in range(3):
+        x0 = torch.randn(M, H, generator=g).to(dev)
+        h = torch.zeros(M, I, dtype=torch.bfloat16, device=dev)
+        ref = x0.clone()
+        Kn.gemm(x0, tgu, h, M, H, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU, splitk=1)
+        Kn.gemm(h, td, ref, M, I, H, epi=_hip.EPI_ADD, splitk=1)
+        outs = []
+        for _ in range(2):
+            x = x0.clone()
+            Kn.mlp_decode(x, M, H, I, tgu, td, 1e-6, ws, err)
+            outs.append(x)
+        assert torch.equal(outs[0], outs[1])
+        torch.testing.assert_close(outs[0], ref, atol=2e-4, rtol=2e-4)
+    assert int(err.item()) == 0
+
+
 def _bf(t):
     return t.to(torch.bfloat16).float()
 

@@ -34,52 +34,57 @@ def timed(fn, label):
     return us
 
 
-ctr = torch.zeros(4, dtype=torch.int32, device=dev)
-timed(lambda: K.advance(ctr, 2), "advance (1 block, trivial)")
-K.gemm_workspace(dev)
-# cold weights: cycle through enough distinct matrices (> 256 MiB Infinity Cache) that every launch streams HBM;
-# split-K off (1) vs auto (0) vs forced factors, same box / same run (QT_GEMV_WPB env caps waves per block)
-shapes = [(1024, 1024), (2048, 1024), (1024, 2048), (4096, 1024), (6144, 1024), (1024, 3072), (2048, 2048),
-          (4096, 2048), (3072, 2048), (12288, 2048), (2048, 6144)]
-for (Nn, Kk) in shapes:
-    nmat = max(2, int(600e6 // (Nn * Kk * 2)))
-    Ws = [K.tile_linear(torch.randn(Nn, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
-    A = torch.randn(8, Kk, device=dev)
-    out = torch.zeros(8, Nn, device=dev)
-    for sk in (1, 0, 2, 4):  # 1 no split, 0 auto, n split-K
-        for rms in ((False, True) if sk in (1, 0) else (False,)):
-            it = {"i": 0}
+def main():
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)
+    timed(lambda: K.advance(ctr, 2), "advance (1 block, trivial)")
+    K.gemm_workspace(dev)
+    # cold weights: cycle through enough distinct matrices (> 256 MiB Infinity Cache) that every launch streams HBM;
+    # split-K off (1) vs auto (0) vs forced factors, same box / same run (QT_GEMV_WPB env caps waves per block)
+    shapes = [(1024, 1024), (2048, 1024), (1024, 2048), (4096, 1024), (6144, 1024), (1024, 3072), (2048, 2048),
+              (4096, 2048), (3072, 2048), (12288, 2048), (2048, 6144)]
+    for (Nn, Kk) in shapes:
+        nmat = max(2, int(600e6 // (Nn * Kk * 2)))
+        Ws = [K.tile_linear(torch.randn(Nn, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
+        A = torch.randn(8, Kk, device=dev)
+        out = torch.zeros(8, Nn, device=dev)
+        for sk in (1, 0, 2, 4):  # 1 no split, 0 auto, n split-K
+            for rms in ((False, True) if sk in (1, 0) else (False,)):
+                it = {"i": 0}
 
-            def f():
-                K.gemm(A, Ws[it["i"] % nmat], out, 8, Kk, Nn, splitk=sk, rms=rms, eps=1e-6)
-                it["i"] += 1
-            us = timed(f, f"COLD gemv M=8 N={Nn} K={Kk} splitk={sk}{' rms' if rms else ''}")
-            if not rms:
-                print(f"{'':60s} -> {Nn * Kk * 2 / us / 1e3:8.1f} GB/s")
-    del Ws
-lg = torch.randn(8, 3072, device=dev)
-tok = torch.zeros(8, dtype=torch.int32, device=dev)
-step = torch.zeros(1, dtype=torch.int32, device=dev)
-seen = torch.zeros(8, 3072, dtype=torch.uint8, device=dev)
-timed(lambda: K.sample(lg, 8, 3072, 3072, tok), "sample greedy V=3072")
-timed(lambda: K.sample(lg, 8, 3072, 3072, tok, seen=seen, rep_penalty=1.05, n_generated=step, min_new_tokens=2,
-                       eos_id=2150, suppress=(2048, 3072, 2150)), "sample greedy + processors")
-timed(lambda: K.sample(lg, 8, 3072, 3072, tok, do_sample=True, top_k=50, temperature=0.9, step=step, seed=1),
-      "sample top-k 50 V=3072")
-timed(lambda: K.sample(lg, 8, 3072, 3072, tok, do_sample=True, top_k=0, temperature=0.9, step=step, seed=1),
-      "sample no-top-k V=3072")
-timed(lambda: K.sample(lg[:, :2048].contiguous(), 8, 2048, 2048, tok, do_sample=True, top_k=50, temperature=0.9,
-                       step=step, seed=1), "sample top-k 50 V=2048")
-# decode attention
-for L in (17, 300):
-    B, Hq, Hkv, D = 8, 16, 8, 128
-    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev)
-    kc = torch.randn(B, Hkv, L + 4, D, device=dev).bfloat16()
-    vc = torch.randn(B, Hkv, L + 4, D, device=dev).bfloat16()
-    qn = torch.ones(D, device=dev)
-    cos, sin = K.rope_tables(D, 1e6, 4096, dev)
-    i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
-    pos, rb, st = i32([L - 1] * B), i32(range(B)), i32([0] * B)
-    out = torch.zeros(B, Hq * D, device=dev)
-    timed(lambda: K.decode_attention(qkv, B, Hq, Hkv, D, qn, qn, 1e-6, cos, sin, pos, rb, pos, st, kc, vc, L + 4, out),
-          f"decode attention B=8 L={L}")
+                def f():
+                    K.gemm(A, Ws[it["i"] % nmat], out, 8, Kk, Nn, splitk=sk, rms=rms, eps=1e-6)
+                    it["i"] += 1
+                us = timed(f, f"COLD gemv M=8 N={Nn} K={Kk} splitk={sk}{' rms' if rms else ''}")
+                if not rms:
+                    print(f"{'':60s} -> {Nn * Kk * 2 / us / 1e3:8.1f} GB/s")
+        del Ws
+    lg = torch.randn(8, 3072, device=dev)
+    tok = torch.zeros(8, dtype=torch.int32, device=dev)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    seen = torch.zeros(8, 3072, dtype=torch.uint8, device=dev)
+    timed(lambda: K.sample(lg, 8, 3072, 3072, tok), "sample greedy V=3072")
+    timed(lambda: K.sample(lg, 8, 3072, 3072, tok, seen=seen, rep_penalty=1.05, n_generated=step, min_new_tokens=2,
+                           eos_id=2150, suppress=(2048, 3072, 2150)), "sample greedy + processors")
+    timed(lambda: K.sample(lg, 8, 3072, 3072, tok, do_sample=True, top_k=50, temperature=0.9, step=step, seed=1),
+          "sample top-k 50 V=3072")
+    timed(lambda: K.sample(lg, 8, 3072, 3072, tok, do_sample=True, top_k=0, temperature=0.9, step=step, seed=1),
+          "sample no-top-k V=3072")
+    timed(lambda: K.sample(lg[:, :2048].contiguous(), 8, 2048, 2048, tok, do_sample=True, top_k=50, temperature=0.9,
+                           step=step, seed=1), "sample top-k 50 V=2048")
+    # decode attention
+    for L in (17, 300):
+        B, Hq, Hkv, D = 8, 16, 8, 128
+        qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev)
+        kc = torch.randn(B, Hkv, L + 4, D, device=dev).bfloat16()
+        vc = torch.randn(B, Hkv, L + 4, D, device=dev).bfloat16()
+        qn = torch.ones(D, device=dev)
+        cos, sin = K.rope_tables(D, 1e6, 4096, dev)
+        i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
+        pos, rb, st = i32([L - 1] * B), i32(range(B)), i32([0] * B)
+        out = torch.zeros(B, Hq * D, device=dev)
+        timed(lambda: K.decode_attention(qkv, B, Hq, Hkv, D, qn, qn, 1e-6, cos, sin, pos, rb, pos, st, kc, vc, L + 4, out),
+              f"decode attention B=8 L={L}")
+
+
+if __name__ == "__main__":
+    main()
