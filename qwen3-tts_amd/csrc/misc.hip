@@ -68,7 +68,8 @@ __global__ void rvq_gather_k(const float* __restrict__ tabs, int Q, int n_first,
   for (int i = threadIdx.x; i < dim; i += blockDim.x) {
     float s1 = 0.f, s2 = 0.f;
     for (int q = 0; q < Q; ++q) {
-      float v = tabs[((long long)q * cb + c[q]) * dim + i];
+      const int code = min(max(c[q], 0), cb - 1);  // callers validate; never read outside the table
+      float v = tabs[((long long)q * cb + code) * dim + i];
       if (q < n_first) s1 += v; else s2 += v;
     }
     o1[bt * dim + i] = s1;

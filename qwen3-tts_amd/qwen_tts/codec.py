@@ -215,6 +215,11 @@ class CodecDecoder:
 
     def decode(self, audio_codes: torch.Tensor) -> List[torch.Tensor]:
         """Qwen3TTSTokenizerV2Model.decode (K:992-1022): [B, T, 16] -> list of 1-D fp32 wavs (device)."""
+        cb = self.tables.shape[1]
+        if audio_codes.numel() and (int(audio_codes.min()) < 0 or int(audio_codes.max()) >= cb):
+            # the reference's codebook lookup raises on such ids (nn.Embedding / F.embedding IndexError)
+            raise ValueError(f"audio codes must lie in [0, {cb}); got [{int(audio_codes.min())}, "
+                             f"{int(audio_codes.max())}]")
         if audio_codes.shape[1] == 0:
             return [torch.zeros(0, device=self.dev) for _ in range(audio_codes.shape[0])]
         wav = self.chunked_decode(audio_codes)

@@ -259,12 +259,20 @@ class Qwen3TTSModel:
         return self._decode(codes)
 
     @torch.no_grad()
-    def stream(self, text, speaker=None, language=None, instruct=None, non_streaming_mode=True, **kwargs):
-        """New surface (no reference counterpart): yields (utterance index, pcm, sr) for each
-        utterance of a custom-voice batch as soon as its codes are complete and decoded."""
-        wavs, sr = self.generate_custom_voice(text, speaker, language, instruct, non_streaming_mode, **kwargs)
-        for i, w in enumerate(wavs):
-            yield i, w, sr
+    def stream(self, text, speaker=None, language=None, instruct=None, non_streaming_mode=True,
+               first_chunk_frames=12, chunk_frames=48, left_context=25, **kwargs):
+        """New surface (no reference counterpart): streaming custom-voice generation.
+        Yields (utterance index, pcm chunk np.float32, sample rate, is_last) while the batch decodes: the first
+        chunk after `first_chunk_frames` frames (~1 s of audio), then every `chunk_frames`.  Per utterance the
+        chunks concatenate to the one-shot generate_custom_voice() length; codes are identical to it (see
+        TTSModel.stream for the chunk / left-context rule)."""
+        input_ids, ins_ids, languages, speakers = self._custom_voice_inputs(text, speaker, language, instruct)
+        sr = self.model.speech_tokenizer.get_output_sample_rate()
+        for i, pcm, last in self.model.stream(input_ids=input_ids, instruct_ids=ins_ids, languages=languages,
+                                              speakers=speakers, non_streaming_mode=non_streaming_mode,
+                                              first_chunk_frames=first_chunk_frames, chunk_frames=chunk_frames,
+                                              left_context=left_context, **self._merge_generate_kwargs(**kwargs)):
+            yield i, pcm.to(torch.float32).cpu().numpy(), sr, last
 
     def get_supported_speakers(self) -> Optional[List[str]]:
         s = self._supported_speakers_set()

@@ -322,6 +322,19 @@ class TalkerEngine:
         The batch is decoded as `groups` independent row groups (default self.row_groups), each on its own
         HIP stream with its own session and captured frame graph; per-row arithmetic (and, through row_base,
         each row's Philox stream) is the same as decoding the batch whole."""
+        it = self.decode_iter(embeds, mask, trailing, tts_pad, gp, use_graph=use_graph, on_frames=on_frames,
+                              groups=groups)
+        sessions, frames = None, 0
+        for sessions, frames, _ in it:
+            pass
+        return self.collect(sessions, frames)
+
+    def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
+                    groups: Optional[int] = None, every: int = 0, first: int = 0):
+        """Prefill + frame loop as a generator: yields (sessions, frames_done, final) after `first` frames, then
+        every `every` frames (0: only at the end), and once at the end with final=True.  codes[:, :frames_done]
+        of every session are final when yielded (device; the yield synchronises the row-group streams), and
+        codes[:, frames_done, 0] already holds the next frame's cb0 (EOS of rows that just finished)."""
         B, P, H = embeds.shape
         G = max(1, min(groups or self.row_groups, B))
         max_frames = max(gp.max_new_tokens - 1, 0)
@@ -341,6 +354,7 @@ class TalkerEngine:
             streams.append(st)
         frames = 0
         check_every = 8
+        next_yield = first or every
         while frames < max_frames:
             for s, st in zip(sessions, streams):
                 with torch.cuda.stream(st):
@@ -353,6 +367,11 @@ class TalkerEngine:
             frames += 1
             if on_frames is not None:
                 on_frames(sessions[0], frames)
+            if next_yield and frames == next_yield and frames < max_frames:
+                for st in streams:
+                    main.wait_stream(st)
+                yield sessions, frames, False
+                next_yield = frames + every if every else 0
             if frames % check_every == 0 or frames == max_frames:
                 if all(bool(s.finished.all()) for s in sessions):
                     break
@@ -362,6 +381,10 @@ class TalkerEngine:
             for sc in (s.sc_t, s.sc_c):
                 if "mlp_err" in sc and int(sc["mlp_err"].item()):
                     raise RuntimeError("qt_mlp_decode: in-kernel arrival wait timed out (results invalid)")
+        yield sessions, frames, True
+
+    def collect(self, sessions, frames):
+        """Per-row codes (EOS-truncated, M:2280-2292) and last hidden states, host tensors."""
         eos = self.tc["codec_eos_token_id"]
         out_c, out_h = [], []
         for s in sessions:

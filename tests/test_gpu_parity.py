@@ -507,6 +507,50 @@ def test_row_groups_identical_to_whole_batch(tiny_models, dtype):
             np.testing.assert_array_equal(a.numpy(), b.numpy())
 
 
+@pytest.mark.parametrize("ctx,eos", [(1000, False), (1000, True), (2, True)])
+def test_stream_matches_one_shot(tiny_models, ctx, eos):
+    """stream(): per utterance the PCM chunks concatenate to exactly the one-shot generate+decode length
+    (EOS-ragged batch included); with left context covering the utterance they equal the one-shot PCM; the
+    first chunk (no left context needed) always does."""
+    from cases import gen_kwargs, make_inputs, talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    from qwen_tts.model import TTSModel
+    _dev()
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    W = dict(W)
+    if eos:
+        z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+        head = W["talker.codec_head.weight"].clone()
+        head[cfg["talker_config"]["codec_eos_token_id"]] = head[int(z["eos_b2/donor"])]
+        W["talker.codec_head.weight"] = head
+    model = TTSModel(cfg, W, dtype="fp32")
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    tok = Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer", dtype="fp32", weights=CW)
+    model.load_speech_tokenizer(tok)
+    key = "cv_b2_stream_dialect"
+    case = dict(talker_cases()[key], max_new_tokens=24 if eos else 30)
+    ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
+    kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=case["languages"],
+              speakers=case["speakers"], non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+    codes, _ = model.generate(**kw)
+    wavs, _ = tok.decode([{"audio_codes": c} for c in codes])
+    if eos:
+        assert len({c.shape[0] for c in codes}) > 1  # ragged: rows stop at different frames
+    chunks = {}
+    for b, pcm, last in model.stream(first_chunk_frames=3, chunk_frames=5, left_context=ctx, **kw):
+        chunks.setdefault(b, []).append(pcm.cpu().numpy())
+    assert sorted(chunks) == list(range(len(codes)))
+    for b, w in enumerate(wavs):
+        got = np.concatenate(chunks[b])
+        assert got.shape == w.shape, (b, got.shape, w.shape)
+        first = chunks[b][0]
+        np.testing.assert_allclose(first, w[:first.shape[0]], atol=2e-4, rtol=0)
+        if ctx >= 1000:
+            np.testing.assert_allclose(got, w, atol=2e-4, rtol=0)
+
+
 def test_talker_bf16_runs_and_tracks_fp32(tiny_models):
     from cases import talker_cases
     from qwen_tts.model import TTSModel
