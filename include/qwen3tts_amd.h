@@ -167,6 +167,9 @@ typedef struct qt_sample_args {
   int* tok_out;
   int* codes; long long codes_ld; int codes_w; int codes_col; int codes_step_off;
   int row_base;  /* global index of row 0: Philox stream id = row_base + r, so a batch split into row groups draws exactly the streams of the whole batch */
+  /* optional next-step input: emb_out[r*emb_ld + i] = emb_table[tok*emb_dim + i], i < emb_dim (fp32) -- the
+   * embedding of the chosen token (pre-projected when the model has small_to_mtp), written by the sampler */
+  const float* emb_table; int emb_dim; float* emb_out; long long emb_ld;
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 

@@ -246,8 +246,13 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
       tok = 0;
     }
   }
-  if (tid != 0) return;
   if (fin) tok = p.eos_id;
+  if (p.emb_table) {  // next-step input row: the chosen token's (projected) embedding
+    const float* src = p.emb_table + (long long)tok * p.emb_dim;
+    float* dst = p.emb_out + (long long)r * p.emb_ld;
+    for (int i = tid * 4; i < p.emb_dim; i += NT * 4) *(f32x4_t*)(dst + i) = *(const f32x4_t*)(src + i);
+  }
+  if (tid != 0) return;
   p.tok_out[r] = tok;
   if (p.codes) {
     const int st = (p.step ? *p.step : 0) + p.codes_step_off;
@@ -262,6 +267,7 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
 extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * PER || !a->tok_out) return QT_ERR_SHAPE;
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
+  if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
   hipLaunchKernelGGL(sample_k, dim3(a->R), dim3(NT), 0, (hipStream_t)stream, *a);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }

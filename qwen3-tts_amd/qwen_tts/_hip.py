@@ -64,7 +64,8 @@ class SampleArgs(ctypes.Structure):
                 ("finished", c_void_p), ("do_sample", c_int), ("top_k", c_int), ("top_p", c_float),
                 ("temperature", c_float), ("seed", c_ull), ("step", c_void_p), ("substep", c_int),
                 ("tok_out", c_void_p), ("codes", c_void_p), ("codes_ld", c_ll), ("codes_w", c_int),
-                ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int)]
+                ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int),
+                ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll)]
 
 
 class MlpArgs(ctypes.Structure):

@@ -206,12 +206,26 @@ class TalkerEngine:
                          for g in range(self.G - 1)]  # CP final norm folded in (M:1142, 1299)
         s2m = "talker.code_predictor.small_to_mtp_projection.weight"
         self.s2m = K.tile_linear(_w(W, s2m, dev), wdt, _w(W, s2m.replace("weight", "bias"), dev)) if s2m in W else None
+        # next-step code-predictor inputs as tables (fp32 [vocab][Hc]): codec embedding rows already passed
+        # through small_to_mtp (when present), gathered by the samplers instead of a per-step GEMV
+        Hc = cc["hidden_size"]
+        self.cp_in_tabs = [self._proj_table(self.ecp[g], Hc) for g in range(self.G - 2)]
+        self.cp_in_tab0 = self._proj_table(self.emb0, Hc)
         self._sessions: Dict[tuple, Session] = {}
         self._streams: List[torch.cuda.Stream] = []
         # decode row groups: the batch is split into this many independent groups, each with its own session,
         # HIP stream and captured frame graph; their latency-bound frames overlap on the GPU
         self.row_groups = int(os.environ.get("QT_ROW_GROUPS", "1"))
         torch.cuda.synchronize()
+
+    def _proj_table(self, emb, Hc):
+        """small_to_mtp(embedding table) (M:1299 applied row-wise) or the table itself, fp32 [V][Hc]."""
+        V = emb.shape[0]
+        if self.s2m is None:
+            return emb.float().contiguous()
+        out = torch.empty(V, Hc, dtype=torch.float32, device=self.dev)
+        K.gemm(emb, self.s2m, out, V, emb.shape[1], Hc, a_dtype=emb.dtype)
+        return out
 
     # ---------------------------------------------------------------- G1: prompt embeddings
     def text_proj(self, ids: torch.Tensor) -> torch.Tensor:
@@ -271,29 +285,23 @@ class TalkerEngine:
                  finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
                  temperature=gp.temperature, seed=gp.seed, step=s.step, substep=substep, codes=s.codes,
                  codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off,
-                 row_base=s.row_base)
+                 row_base=s.row_base, emb=(self.cp_in_tab0, s.cp_x.view(-1)[self.cp.H:], 2 * self.cp.H))
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
         B, t, c, gp = s.B, self.talker, self.cp, s.gp
         Hc = c.H
         codes_ld = s.codes.shape[1] * self.G
-        # --- code predictor prefill: rows (2b, 2b+1) = (past_hidden[b], codec_embedding(tok0[b]))
+        # --- code predictor prefill: rows (2b, 2b+1) = (past_hidden[b], codec_embedding(tok0[b])); the odd rows
+        # were written by the talker sampler that chose tok0 (projected embedding table)
         if self.s2m is not None:
             K.gemm(s.past_hidden, self.s2m, s.cp_x, B, t.H, 2 * Hc)
-            K.gemm(self.emb0, self.s2m, s.cp_x.view(-1)[Hc:], B, t.H, 2 * Hc,
-                   a_dtype=self.emb0.dtype, o_dtype=torch.float32, a_index=s.tok0)
         else:
             s.cp_x.view(B, 2, Hc)[:, 0].copy_(s.past_hidden)
-            K.gather_rows(self.emb0, s.tok0, B, Hc, s.cp_x.view(-1)[Hc:], 2 * Hc)
         c.forward(s.cp_x, 2 * B, s.cp_meta0, s.cp_kv, s.sc_c, s.cp_L, s.cp_L)
         self._cp_head(s, s.cp_x.view(-1)[Hc:], 2 * Hc, 0)
         for g in range(1, self.G - 1):
-            x = s.cp_x[:B]
-            if self.s2m is not None:
-                K.gemm(self.ecp[g - 1], self.s2m, x, B, t.H, Hc, a_dtype=self.ecp.dtype, a_index=s.cp_tok)
-            else:
-                K.gather_rows(self.ecp[g - 1], s.cp_tok, B, Hc, x, Hc)
+            x = s.cp_x[:B]  # written by the previous step's sampler (embedding of the token it chose)
             c.forward(x, B, s.cp_meta[g - 1], s.cp_kv, s.sc_c, s.cp_L, s.cp_L, decode=True)
             self._cp_head(s, x, Hc, g)
         # --- talker decode input and forward
@@ -311,7 +319,8 @@ class TalkerEngine:
         K.sample(s.cp_logits, s.B, self.Vc, self.Vc, s.cp_tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed=gp.seed, step=s.step, substep=1 + g, codes=s.codes, codes_ld=s.codes.shape[1] * self.G,
-                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base)
+                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base,
+                 emb=(self.cp_in_tabs[g], s.cp_x, c.H) if g < self.G - 2 else None)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
