@@ -124,7 +124,11 @@ typedef struct qt_decode_attn_args {
   void* out; int o_dtype;  /* [R][Hq*D]; bf16 output = the rounding the next bf16 MFMA applies anyway */
   int const_pos;  /* >= 0: rope_pos = kv_pos = const_pos, row_start = 0, row_batch = r (code-predictor steps:
                      static positions as a launch constant, so no dependent load precedes the K/V stream) */
+  int nsplit;     /* split-KV: each (row, kv head) runs on nsplit blocks over disjoint key ranges (<= 8; 0/1 = off);
+                     the last block to arrive merges the partial softmax states in split order (deterministic) */
+  void* ws; long long ws_bytes;  /* nsplit > 1: zero-initialised scratch >= qt_decode_attn_ws_bytes(), one stream */
 } qt_decode_attn_args;
+long long qt_decode_attn_ws_bytes(int R, int Hq, int Hkv, int D, int nsplit);
 int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

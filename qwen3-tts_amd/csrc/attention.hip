@@ -198,7 +198,7 @@ int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
 template <typename KV, int D, int NREP>
 __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
   constexpr int NW = 8;  // waves: 8 x 64 lanes keeps kf/vf/o/q (~150 VGPRs) out of scratch
-  constexpr int LPK = D / 8, GPW = 64 / LPK, G = NW * GPW, IC = 4;
+  constexpr int LPK = D / 8, GPW = 64 / LPK, G = NW * GPW, IC = sizeof(KV) == 2 ? 4 : 2;
   __shared__ float qs[NREP][D];
   __shared__ float knew[D], vnew[D];
   __shared__ float mrg_ml[NW][NREP][2];
@@ -221,8 +221,9 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
   const KV* Vc = (const KV*)p.v_cache + base;
   // raw fragments stay packed (bf16: 4 VGPRs per 8 elements) until used: IC keys in flight per group
   constexpr int RW = sizeof(KV) * 8 / 4;  // 32-bit words per 8-element fragment
-  unsigned kr[IC][RW], vr[IC][RW];
-  auto load_chunk = [&](int j0) {  // cached keys only; the new key's slot is filled after phase 0
+  unsigned kr[IC][RW], vr[IC][RW];   // chunk being consumed
+  unsigned kn[IC][RW], vn[IC][RW];   // next chunk, in flight while the current one is consumed
+  auto load_into = [&](int j0, unsigned (*kd)[RW], unsigned (*vd)[RW]) {  // cached keys only
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
       const int jj = min(j0 + c * G, max(n - 2, 0));
@@ -231,11 +232,12 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
 #pragma unroll
       for (int q4 = 0; q4 < RW; q4 += 4) {
         u32x4_t a = *(const u32x4_t*)(ks + q4), b = *(const u32x4_t*)(vs + q4);
-        kr[c][q4] = a[0]; kr[c][q4 + 1] = a[1]; kr[c][q4 + 2] = a[2]; kr[c][q4 + 3] = a[3];
-        vr[c][q4] = b[0]; vr[c][q4 + 1] = b[1]; vr[c][q4 + 2] = b[2]; vr[c][q4 + 3] = b[3];
+        kd[c][q4] = a[0]; kd[c][q4 + 1] = a[1]; kd[c][q4 + 2] = a[2]; kd[c][q4 + 3] = a[3];
+        vd[c][q4] = b[0]; vd[c][q4 + 1] = b[1]; vd[c][q4 + 2] = b[2]; vd[c][q4 + 3] = b[3];
       }
     }
   };
+  auto load_chunk = [&](int j0) { load_into(j0, kr, vr); };
   auto unpack = [&](const unsigned* r, float* o8) {
     if constexpr (sizeof(KV) == 2) {
 #pragma unroll
@@ -245,7 +247,11 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
       for (int i = 0; i < 8; ++i) o8[i] = __uint_as_float(r[i]);
     }
   };
-  if (gid < n) load_chunk(gid);  // in flight while phase 0 runs
+  // split-KV: block z of gridDim.z owns keys [j_lo, j_hi) of [0, n) (the new key n-1 is in the last split)
+  const int nsplit = gridDim.z, z = blockIdx.z;
+  const int per_split = (n + nsplit - 1) / nsplit;
+  const int j_lo = min(n, z * per_split), j_hi = min(n, j_lo + per_split);
+  if (j_lo + gid < j_hi) load_chunk(j_lo + gid);  // in flight while phase 0 runs
   // ---- phase 0: norm + rope of q heads / new k, v passthrough; append to cache
   if (w < NREP + 2) {
     const int hh = w < NREP ? h * NREP + w : (w == NREP ? nq + h : nq + nk + h);
@@ -272,7 +278,7 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
         x1 = to_f(from_f<KV>(x1));
       }
       dst[lane] = x0; dst[lane + half] = x1;
-      if (w >= NREP) {
+      if (w >= NREP && z == nsplit - 1) {
         KV* cache = (KV*)(w == NREP ? p.k_cache : p.v_cache) + base + (long long)kvpos * D;
         cache[lane] = from_f<KV>(x0);
         cache[lane + half] = from_f<KV>(x1);
@@ -280,7 +286,8 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
     }
   }
   __syncthreads();
-  const float scale = rsqrtf((float)D);
+  // scores in log2 units: q pre-scaled by log2(e)/sqrt(D), every softmax exponential is one exp2
+  const float scale = rsqrtf((float)D) * 1.4426950408889634f;
   float q[NREP][8];
 #pragma unroll
   for (int j = 0; j < NREP; ++j)
@@ -293,35 +300,58 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[j][i] = 0.f;
   }
-  for (int j0 = gid; j0 < n; j0 += G * IC) {
+  // ping-pong between the two register sets: chunk i is consumed from one while chunk i+1 streams into the
+  // other (no register copies, so no wait on the prefetch before the next chunk's math)
+  // one chunk = IC keys per lane group: all scores first, then one running-max update and one rescale
+  auto consume = [&](auto& kd, auto& vd, const int jb) {
+    float vf[IC][8], dd[NREP][IC];
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
-      const bool valid = j0 + c * G < n;
-      float kf[8], vf[8];
-      unpack(kr[c], kf);
-      unpack(vr[c], vf);
-      if (j0 + c * G >= n - 1) {
+      const bool valid = jb + c * G < j_hi;
+      float kf[8];
+      unpack(kd[c], kf);
+      unpack(vd[c], vf[c]);
+      if (jb + c * G >= n - 1) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { kf[i] = knew[sub * 8 + i]; vf[i] = vnew[sub * 8 + i]; }
+        for (int i = 0; i < 8; ++i) { kf[i] = knew[sub * 8 + i]; vf[c][i] = vnew[sub * 8 + i]; }
       }
 #pragma unroll
       for (int j = 0; j < NREP; ++j) {
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
-#pragma unroll
-        for (int off = LPK / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-        if (valid) {
-          const float mn = fmaxf(m[j], d);
-          const float f = expf(m[j] - mn), e = expf(d - mn);
-          l[j] = l[j] * f + e;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vf[i];
-          m[j] = mn;
-        }
+        d = group_sum_dpp<LPK>(d);  // the key's LPK lanes are one DPP row (or part of one)
+        dd[j][c] = valid ? d : -INFINITY;
       }
     }
-    if (j0 + G * IC < n) load_chunk(j0 + G * IC);
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      float mn = m[j];
+#pragma unroll
+      for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
+      if (mn == -INFINITY) continue;  // no valid key yet in this lane group
+      const float f = exp2f(m[j] - mn);
+      float e[IC], es = 0.f;
+#pragma unroll
+      for (int c = 0; c < IC; ++c) { e[c] = exp2f(dd[j][c] - mn); es += e[c]; }
+      l[j] = l[j] * f + es;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float acc = o[j][i] * f;
+#pragma unroll
+        for (int c = 0; c < IC; ++c) acc += e[c] * vf[c][i];
+        o[j][i] = acc;
+      }
+      m[j] = mn;
+    }
+  };
+  constexpr int GIC = G * IC;
+  for (int j0 = j_lo + gid; j0 < j_hi; j0 += 2 * GIC) {
+    if (j0 + GIC < j_hi) load_into(j0 + GIC, kn, vn);
+    consume(kr, vr, j0);
+    if (j0 + GIC >= j_hi) break;
+    if (j0 + 2 * GIC < j_hi) load_into(j0 + 2 * GIC, kr, vr);
+    consume(kn, vn, j0 + GIC);
   }
   // merge lane groups inside the wave
 #pragma unroll
@@ -330,8 +360,8 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
     for (int j = 0; j < NREP; ++j) {
       const float m2 = __shfl_xor(m[j], off, 64), l2 = __shfl_xor(l[j], off, 64);
       const float mn = fmaxf(m[j], m2);
-      const float f1 = m[j] == -INFINITY ? 0.f : expf(m[j] - mn);
-      const float f2 = m2 == -INFINITY ? 0.f : expf(m2 - mn);
+      const float f1 = m[j] == -INFINITY ? 0.f : exp2f(m[j] - mn);
+      const float f2 = m2 == -INFINITY ? 0.f : exp2f(m2 - mn);
       l[j] = l[j] * f1 + l2 * f2;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -350,6 +380,9 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
     }
   }
   __syncthreads();
+  // split-KV partial record per (row, kv head, split, q head): [m, l, o[0..D)] (unnormalised)
+  constexpr int REC = D + 2;
+  float* part = nsplit > 1 ? (float*)((char*)p.ws + 4096) + (((size_t)r * nk + h) * nsplit) * NREP * REC : nullptr;
   for (int e = tid; e < NREP * D; e += NW * 64) {
     const int j = e / D, d = e % D;
     float mm = -INFINITY;
@@ -357,9 +390,50 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
     float ll = 0.f, oo = 0.f;
     for (int ww = 0; ww < NW; ++ww) {
       const float mw = mrg_ml[ww][j][0];
-      const float f = mw == -INFINITY ? 0.f : expf(mw - mm);
+      const float f = mw == -INFINITY ? 0.f : exp2f(mw - mm);
       ll += mrg_ml[ww][j][1] * f;
       oo += mrg_o[ww][j][d] * f;
+    }
+    if (nsplit > 1) {
+      float* rec = part + ((size_t)z * NREP + j) * REC;
+      __hip_atomic_store(rec + 2 + d, oo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) {
+        __hip_atomic_store(rec, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec + 1, ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    const long long oi = ((long long)r * nq + h * NREP + j) * D + d;
+    if (p.o_dtype == QT_BF16) ((bf16_t*)p.out)[oi] = f2bf(oo / ll);
+    else ((float*)p.out)[oi] = oo / ll;
+  }
+  if (nsplit == 1) return;
+  // the last split to arrive merges all splits in split order (deterministic) and writes the output
+  __shared__ unsigned last_sh;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  unsigned* cnt = (unsigned*)p.ws + (size_t)r * nk + h;
+  if (tid == 0)
+    last_sh = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsplit - 1;
+  __syncthreads();
+  if (!last_sh) return;
+  if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  for (int e = tid; e < NREP * D; e += NW * 64) {
+    const int j = e / D, d = e % D;
+    float ms[8], ls[8], os[8];  // nsplit <= 8
+    float mm = -INFINITY;
+    for (int zz = 0; zz < nsplit; ++zz) {
+      const float* rec = part + ((size_t)zz * NREP + j) * REC;
+      ms[zz] = __hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ls[zz] = __hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      os[zz] = __hip_atomic_load(rec + 2 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int zz = 0; zz < nsplit; ++zz) mm = fmaxf(mm, ms[zz]);
+    float ll = 0.f, oo = 0.f;
+    for (int zz = 0; zz < nsplit; ++zz) {
+      const float f = ms[zz] == -INFINITY ? 0.f : exp2f(ms[zz] - mm);
+      ll += ls[zz] * f;
+      oo += os[zz] * f;
     }
     const long long oi = ((long long)r * nq + h * NREP + j) * D + d;
     if (p.o_dtype == QT_BF16) ((bf16_t*)p.out)[oi] = f2bf(oo / ll);
@@ -367,9 +441,17 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
   }
 }
 
+}  // namespace
+extern "C" long long qt_decode_attn_ws_bytes(int R, int Hq, int Hkv, int D, int nsplit);
+namespace {
+
 template <typename KV, int D>
 int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
-  dim3 g(a.R, a.Hkv);
+  const int ns = a.nsplit > 1 ? a.nsplit : 1;
+  if (ns > 8) return QT_ERR_ARG;
+  if (ns > 1 && (!a.ws || a.ws_bytes < qt_decode_attn_ws_bytes(a.R, a.Hq, a.Hkv, a.D, ns))) return QT_ERR_ARG;
+  if (ns > 1 && a.R * a.Hkv > 1024) return QT_ERR_SHAPE;  // arrival counters live in the 4 KiB header
+  dim3 g(a.R, a.Hkv, ns);
   switch (a.Hq / a.Hkv) {
     case 1: hipLaunchKernelGGL((attn_decode_k<KV, D, 1>), g, dim3(512), 0, s, a); break;
     case 2: hipLaunchKernelGGL((attn_decode_k<KV, D, 2>), g, dim3(512), 0, s, a); break;
@@ -400,6 +482,10 @@ extern "C" int qt_attention(const qt_attn_args* a, void* stream) {
   if (a->kv_dtype == QT_BF16 && a->o_dtype == QT_BF16) return attn_dispatch<bf16_t, bf16_t>(*a, s);
   if (a->kv_dtype == QT_F32 && a->o_dtype == QT_F32) return attn_dispatch<float, float>(*a, s);
   return QT_ERR_DTYPE;
+}
+
+extern "C" long long qt_decode_attn_ws_bytes(int R, int Hq, int Hkv, int D, int nsplit) {
+  return 4096 + (long long)R * Hq * nsplit * (D + 2) * (long long)sizeof(float);
 }
 
 extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {

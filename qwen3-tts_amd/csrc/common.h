@@ -53,6 +53,20 @@ QT_DEV int wave_sum_i(int v) {
          __builtin_amdgcn_readlane(v, 48);
 }
 
+// Sum over aligned groups of N (2, 4, 8 or 16) lanes, result in every lane of the group: DPP inside a row.
+template <int CTRL>
+QT_DEV float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int N>
+QT_DEV float group_sum_dpp(float v) {
+  if constexpr (N >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (N >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (N >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
+  if constexpr (N >= 16) v += dpp_f<0x140>(v); // row_mirror
+  return v;
+}
+
 QT_DEV float silu_f(float g) { return g / (1.0f + expf(-g)); }
 QT_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 

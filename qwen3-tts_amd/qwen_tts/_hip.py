@@ -54,7 +54,8 @@ class DecodeAttnArgs(ctypes.Structure):
                 ("qkv", c_void_p), ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float),
                 ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("row_batch", c_void_p),
                 ("kv_pos", c_void_p), ("row_start", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
-                ("kv_dtype", c_int), ("out", c_void_p), ("o_dtype", c_int), ("const_pos", c_int)]
+                ("kv_dtype", c_int), ("out", c_void_p), ("o_dtype", c_int), ("const_pos", c_int), ("nsplit", c_int),
+                ("ws", c_void_p), ("ws_bytes", c_ll)]
 
 
 class SampleArgs(ctypes.Structure):
@@ -73,7 +74,8 @@ class MlpArgs(ctypes.Structure):
                 ("w_down", c_void_p), ("eps", c_float), ("ws", c_void_p), ("ws_bytes", c_ll), ("err", c_void_p)]
 
 
-EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_mlp_ws_bytes",
+EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
+           "qt_mlp_ws_bytes",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
 
@@ -98,11 +100,12 @@ def load_library(path: str = LIB_PATH):
         "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
         "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
+        "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
     }
     for name, args in sig.items():
         f = getattr(L, name)
         f.argtypes = args
-        f.restype = c_ll if name == "qt_mlp_ws_bytes" else c_int
+        f.restype = c_ll if name.endswith("_ws_bytes") else c_int
     return L
 
 

@@ -201,8 +201,13 @@ def attention(q, R, Hq, Hkv, D, kc, vc, Lmax, row_batch, row_start, row_len, out
     check(_hip.lib().qt_attention(ctypes.byref(a), stream()), "qt_attention")
 
 
+def decode_attn_ws_bytes(R, Hq, Hkv, D, nsplit):
+    return int(_hip.lib().qt_decode_attn_ws_bytes(R, Hq, Hkv, D, nsplit))
+
+
 def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, row_start,
-                     kc, vc, Lmax, out, window=0, const_pos=-1):
+                     kc, vc, Lmax, out, window=0, const_pos=-1, nsplit=1, ws=None):
+    """nsplit > 1: split-KV over nsplit blocks per (row, kv head); ws from decode_attn_ws_bytes (zeroed)."""
     a = _hip.DecodeAttnArgs()
     a.R, a.Hq, a.Hkv, a.D, a.Lmax, a.window = R, Hq, Hkv, D, Lmax, window
     a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
@@ -211,6 +216,9 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
     a.k_cache, a.v_cache, a.kv_dtype, a.out = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype), ptr(out)
     a.o_dtype = _hip.dtype_code(out.dtype)
     a.const_pos = const_pos
+    a.nsplit = nsplit
+    if ws is not None:
+        a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
     check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
 
 

@@ -342,6 +342,19 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
     Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, same, rb, same, zero, kc5, vc5, L + 3, a5,
                         const_pos=L - 1)
     assert torch.equal(a4, a5) and torch.equal(kc4, kc5) and torch.equal(vc4, vc5)
+    # split-KV (nsplit blocks per (row, kv head), deterministic merge) == single block, bitwise reproducible
+    for ns in (2, 3, 8):
+        ws = torch.zeros(Kn.decode_attn_ws_bytes(B, hq, hkv, D, ns), dtype=torch.uint8, device=dev)
+        outs = []
+        for _ in range(2):
+            kc6, vc6 = kc.clone(), vc.clone()
+            a6 = torch.zeros(B, hq * D, device=dev)
+            Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, kvpos, start, kc6, vc6, L + 3, a6,
+                                nsplit=ns, ws=ws)
+            outs.append(a6)
+            assert torch.equal(kc6, kc2) and torch.equal(vc6, vc2)
+        assert torch.equal(outs[0], outs[1])
+        torch.testing.assert_close(outs[0], a2, atol=tol, rtol=tol)
 
 
 def test_sample_greedy_processors():

@@ -72,7 +72,7 @@ def main():
     timed(lambda: K.sample(lg[:, :2048].contiguous(), 8, 2048, 2048, tok, do_sample=True, top_k=50, temperature=0.9,
                            step=step, seed=1), "sample top-k 50 V=2048")
     # decode attention
-    for L in (17, 300):
+    for L in (17, 300, 460):
         B, Hq, Hkv, D = 8, 16, 8, 128
         qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev)
         kc = torch.randn(B, Hkv, L + 4, D, device=dev).bfloat16()
@@ -82,8 +82,10 @@ def main():
         i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
         pos, rb, st = i32([L - 1] * B), i32(range(B)), i32([0] * B)
         out = torch.zeros(B, Hq * D, device=dev)
-        timed(lambda: K.decode_attention(qkv, B, Hq, Hkv, D, qn, qn, 1e-6, cos, sin, pos, rb, pos, st, kc, vc, L + 4, out),
-              f"decode attention B=8 L={L}")
+        for ns in (1, 2, 4, 8):
+            ws = torch.zeros(K.decode_attn_ws_bytes(B, Hq, Hkv, D, ns), dtype=torch.uint8, device=dev)
+            timed(lambda: K.decode_attention(qkv, B, Hq, Hkv, D, qn, qn, 1e-6, cos, sin, pos, rb, pos, st, kc, vc, L + 4,
+                                             out, nsplit=ns, ws=ws), f"decode attention B=8 L={L} nsplit={ns}")
 
 
 if __name__ == "__main__":
