@@ -342,8 +342,8 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 }
 
 // LDS-tiled implicit GEMM for large M with bf16 weights (codec convs / transposed convs as taps, prefill
-// linears as taps = 1).  Block = 128 output rows x 64 columns, 4 waves; wave w owns rows [32w, 32w+32) x all
-// 64 columns = 2 x 4 MFMA 16x16x32 tiles.  A tile's rows are one batch item's consecutive time steps, so the
+// linears as taps = 1).  Block = 128 output rows x NT*16 columns (NT = 6 or 8), 4 waves; wave w owns rows
+// [32w, 32w+32) x all the block's columns = 2 x NT MFMA 16x16x32 tiles.  A tile's rows are one batch item's consecutive time steps, so the
 // input window [t0 + t_off, t0 + t_off + 127 + (taps-1)*dil] x 32 channels is staged into LDS once per channel
 // chunk (optional SnakeBeta applied while staging, rounded to bf16 like the MFMA operand) and every tap reads
 // its shifted rows from it: the im2col expansion (taps x) never leaves the CU.  The next chunk is loaded into
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 constexpr int IG_BM = 128, IG_BN = 64, IG_KC = 32, IG_LDSW = 40;  // LDS row stride 40 bf16 (80 B)
 constexpr int IG_GPT = 3;  // staged 8-channel groups per thread (window rows <= 192)
 
-template <typename AT, typename OT>
+template <typename AT, typename OT, int NT>
 __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   extern __shared__ unsigned char ig_smem[];
   bf16_t* win = (bf16_t*)ig_smem;  // [2][WR][IG_LDSW]
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   const int WR = IG_BM + (taps - 1) * dil;
   const int tiles_t = (t_out + IG_BM - 1) / IG_BM;
   const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * IG_BM;
-  const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * 4;
+  const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * NT;
   const int nch = cin_pad / IG_KC, ktiles = p.Kp / IG_KC;
   const AT* A = (const AT*)p.A + (long long)bi * t_in * p.lda;
   const bool norm = p.rms != 0;
@@ -394,9 +394,12 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       const int q = tid + i * 256, r = q >> 2, ch = c * IG_KC + (q & 3) * 8;
       if (r >= WR) continue;
       float* v = stg[i];
-      if (p.sn_a && ch < cin) {
+      if (p.sn_a && ch < cin) {  // bf16 operand: the hardware sine's error is far below the bf16 rounding
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = snake1(v[e], p.sn_a[ch + e], p.sn_ib[ch + e]);
+        for (int e = 0; e < 8; ++e) {
+          const float sn = __sinf(v[e] * p.sn_a[ch + e]);
+          v[e] = v[e] + p.sn_ib[ch + e] * (sn * sn);
+        }
       }
       if (norm) {
 #pragma unroll
@@ -407,15 +410,15 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
     }
   };
 
-  f32x4_t acc[2][4];
+  f32x4_t acc[2][NT];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const bf16_t* Wb = (const bf16_t*)p.W + lane * 8;
   auto load_b = [&](u32x4_t* bf, int kt) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NT; ++j) {
       const int nt = min(nt0 + j, ntl - 1);
       bf[j] = *(const u32x4_t*)(Wb + ((size_t)nt * ktiles + kt) * 512);
     }
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   load_chunk(0);
   store_chunk(0, 0);
   __syncthreads();
-  u32x4_t bcur[4], bnxt[4];
+  u32x4_t bcur[NT], bnxt[NT];
   load_b(bcur, 0);  // tap 0 of chunk 0 (k tile = tap * nch + chunk)
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
@@ -440,11 +443,11 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < NT; ++q)
           acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
                                                               __builtin_bit_cast(bf16x8_t, bcur[q]), acc[i][q], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bcur[q] = bnxt[q];
+      for (int q = 0; q < NT; ++q) bcur[q] = bnxt[q];
     }
     if (c + 1 < nch) store_chunk(buf ^ 1, c + 1);
     __syncthreads();
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NT; ++q) {
       const int nt = nt0 + q;
       if (nt >= ntl) continue;
       const int n = nt * 16 + lm;
@@ -594,8 +597,12 @@ int launch(const GemmP& p, hipStream_t s) {
     const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;
     const int WR = IG_BM + (taps - 1) * dil;
     const size_t smem = (size_t)2 * WR * IG_LDSW * sizeof(bf16_t);
-    dim3 grid(batches * ((t_out + IG_BM - 1) / IG_BM), (nt + 3) / 4);
-    hipLaunchKernelGGL((igemm_k<AT, OT>), grid, dim3(256), smem, s, p);
+    // column tile per block: 6 x 16 for 96 / 192-channel layers (no idle tiles, the snake-staged window is
+    // shared by all of a row tile's columns), else 8 x 16
+    const int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8;
+    dim3 grid(batches * ((t_out + IG_BM - 1) / IG_BM), (nt + ntb - 1) / ntb);
+    if (ntb == 6) hipLaunchKernelGGL((igemm_k<AT, OT, 6>), grid, dim3(256), smem, s, p);
+    else hipLaunchKernelGGL((igemm_k<AT, OT, 8>), grid, dim3(256), smem, s, p);
   } else if (p.M <= 32) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 2, 8>), dim3(nt, (p.M + 31) / 32), dim3(512), 0, s, p);
   } else {
