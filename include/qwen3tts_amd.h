@@ -179,6 +179,10 @@ int qt_sample(const qt_sample_args* args, void* stream);
 
 /* Qwen3TTSRMSNorm (M:595-610 / K:372-390): out = gamma * (x * rsqrt(mean(x^2) + eps)), fp32 [M][N]. */
 int qt_rmsnorm(const float* x, const float* gamma, float eps, float* out, int M, int N, void* stream);
+/* qt_rmsnorm + a record of each normalised row at rec[m*rec_ld + (*step + step_off)*N] (per-frame hidden states
+ * written inside the captured frame graph at the device step counter). */
+int qt_rmsnorm_rec(const float* x, const float* gamma, float eps, float* out, int M, int N, float* rec,
+                   long long rec_ld, const int* step, int step_off, void* stream);
 
 /* out[m] = table[idx[m]] (fp32 out, table dtype), nn.Embedding row gather (M:1441, 1670). */
 int qt_gather_rows(const void* table, int dtype, const int* idx, int M, int H, float* out, long long ldo, void* stream);

@@ -6,7 +6,9 @@
 namespace {
 
 __global__ __launch_bounds__(256) void rmsnorm_k(const float* __restrict__ x, const float* __restrict__ g, float eps,
-                                                 float* __restrict__ out, int N) {
+                                                 float* __restrict__ out, int N, float* __restrict__ rec = nullptr,
+                                                 long long rec_ld = 0, const int* __restrict__ step = nullptr,
+                                                 int step_off = 0) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   const float* xr = x + (long long)m * N;
@@ -16,7 +18,12 @@ __global__ __launch_bounds__(256) void rmsnorm_k(const float* __restrict__ x, co
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
   const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
-  for (int i = tid; i < N; i += 256) out[(long long)m * N + i] = g[i] * (xr[i] * rs);
+  float* rr = rec ? rec + (long long)m * rec_ld + (long long)(*step + step_off) * N : nullptr;
+  for (int i = tid; i < N; i += 256) {
+    const float v = g[i] * (xr[i] * rs);
+    out[(long long)m * N + i] = v;
+    if (rr) rr[i] = v;
+  }
 }
 
 template <typename T>
@@ -145,6 +152,13 @@ inline unsigned grid_for(long long n, int bs) {
 extern "C" int qt_rmsnorm(const float* x, const float* g, float eps, float* out, int M, int N, void* s) {
   if (M <= 0 || N <= 0) return QT_ERR_SHAPE;
   hipLaunchKernelGGL(rmsnorm_k, dim3(M), dim3(256), 0, (hipStream_t)s, x, g, eps, out, N);
+  return ok();
+}
+
+extern "C" int qt_rmsnorm_rec(const float* x, const float* g, float eps, float* out, int M, int N, float* rec,
+                              long long rec_ld, const int* step, int step_off, void* s) {
+  if (M <= 0 || N <= 0 || !rec || !step) return QT_ERR_SHAPE;
+  hipLaunchKernelGGL(rmsnorm_k, dim3(M), dim3(256), 0, (hipStream_t)s, x, g, eps, out, N, rec, rec_ld, step, step_off);
   return ok();
 }
 

@@ -242,8 +242,13 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 
-def rmsnorm(x, g, eps, out, M, N):
-    check(_hip.lib().qt_rmsnorm(ptr(x), ptr(g), eps, ptr(out), M, N, stream()), "qt_rmsnorm")
+def rmsnorm(x, g, eps, out, M, N, rec=None, step=None, step_off=0):
+    """rec: also store the rows at rec[m, *step + step_off] (rec [M][F][N] fp32, step a device int32 counter)."""
+    if rec is None:
+        check(_hip.lib().qt_rmsnorm(ptr(x), ptr(g), eps, ptr(out), M, N, stream()), "qt_rmsnorm")
+    else:
+        check(_hip.lib().qt_rmsnorm_rec(ptr(x), ptr(g), eps, ptr(out), M, N, ptr(rec), rec.stride(0), ptr(step),
+                                        step_off, stream()), "qt_rmsnorm_rec")
 
 
 def gather_rows(table, idx, M, H, out, ldo):

@@ -308,7 +308,8 @@ class TalkerEngine:
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B)
         t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True)
-        K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H)
+        # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])
+        K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
         self._sample_talker(s, s.logits, 1, 0)
         K.advance(s.ctr, 2 + 3 * B)
@@ -364,10 +365,15 @@ class TalkerEngine:
         frames = 0
         check_every = 8
         next_yield = first or every
+        for s, st in zip(sessions, streams):
+            with torch.cuda.stream(st):
+                s.hiddens[:, 0].copy_(s.past_hidden)  # later frames are recorded inside the frame graph
+        # EOS polling without a host sync: every `check_every` frames the all-finished flag is copied to pinned
+        # memory behind an event; the copy from the previous window is read once its event has completed
+        pending = []
         while frames < max_frames:
             for s, st in zip(sessions, streams):
                 with torch.cuda.stream(st):
-                    s.hiddens[:, frames].copy_(s.past_hidden)
                     if use_graph:
                         s.graph.replay()
                     else:
@@ -381,8 +387,21 @@ class TalkerEngine:
                     main.wait_stream(st)
                 yield sessions, frames, False
                 next_yield = frames + every if every else 0
-            if frames % check_every == 0 or frames == max_frames:
-                if all(bool(s.finished.all()) for s in sessions):
+            if frames % check_every == 0 and frames < max_frames:
+                flags = []
+                for s, st in zip(sessions, streams):
+                    with torch.cuda.stream(st):
+                        f = torch.empty(1, dtype=torch.bool, pin_memory=True)
+                        f.copy_(s.finished.all().reshape(1), non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(st)
+                        flags.append((f, ev))
+                pending.append(flags)
+                done = False
+                while pending and all(ev.query() for _, ev in pending[0]):
+                    if all(bool(f.item()) for f, _ in pending.pop(0)):
+                        done = True
+                if done:
                     break
         for st in streams:
             main.wait_stream(st)
