@@ -130,6 +130,11 @@ typedef struct qt_decode_attn_args {
 } qt_decode_attn_args;
 long long qt_decode_attn_ws_bytes(int R, int Hq, int Hkv, int D, int nsplit);
 int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
+/* Short prefill whose keys are all new (the code predictor's per-frame 2-token prefill, M:1142-1160): rows
+ * r = b*T + t at positions t = 0..T-1 of batch item b (T == 2), causal over the T keys, k/v appended to the
+ * cache at 0..T-1.  Uses R, Hq, Hkv, D, Lmax, qkv, q_norm, k_norm, eps, cos/sin, caches, out, o_dtype of args.
+ * One launch instead of qt_qkv_post + qt_attention. */
+int qt_small_prefill_attention(const qt_decode_attn_args* args, int T, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * qt_mlp_decode: one decode step of the Qwen3 MLP with its residual, fused (M:655-668: down_proj(act(gate_proj

@@ -445,6 +445,92 @@ __global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
 extern "C" long long qt_decode_attn_ws_bytes(int R, int Hq, int Hkv, int D, int nsplit);
 namespace {
 
+// Short prefill where every key is new (code-predictor per-frame 2-token prefill, positions 0..T-1 of each
+// batch item): one block per (batch item, kv head), one wave per (token, q head | k | v) for the q/k-norm +
+// RoPE + cache append (as qkv_post_k), then one wave per (token, q head) for the causal softmax over the
+// block's own T keys held in LDS.  Replaces qt_qkv_post + qt_attention (two launches) for this case.
+template <typename KV, int D, int NREP, int T>
+__global__ __launch_bounds__(64 * T * (NREP + 2)) void attn_small_prefill_k(qt_decode_attn_args p) {
+  constexpr int half = D / 2;
+  __shared__ float qs[T][NREP][D], ks[T][D], vs[T][D];
+  const int b = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nq = p.Hq, nk = p.Hkv;
+  {
+    const int t = w / (NREP + 2), role = w % (NREP + 2);
+    const int r = b * T + t;
+    const int hh = role < NREP ? h * NREP + role : (role == NREP ? nq + h : nq + nk + h);
+    const float* src = p.qkv + (long long)r * (nq + 2 * nk) * D + (long long)hh * D;
+    const bool act = lane < half;
+    float x0 = act ? src[lane] : 0.f, x1 = act ? src[lane + half] : 0.f;
+    if (role <= NREP) {
+      const float* nw = role < NREP ? p.q_norm : p.k_norm;
+      if (nw) {
+        const float rs = rsqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + p.eps);
+        if (act) { x0 = nw[lane] * (x0 * rs); x1 = nw[lane + half] * (x1 * rs); }
+      }
+      if (act) {
+        const float c = p.cos_tab[(long long)t * half + lane], sn = p.sin_tab[(long long)t * half + lane];
+        const float y0 = x0 * c - x1 * sn, y1 = x1 * c + x0 * sn;
+        x0 = y0; x1 = y1;
+      }
+    }
+    if (act) {
+      if (role < NREP) {
+        qs[t][role][lane] = x0; qs[t][role][lane + half] = x1;
+      } else {  // as the cache holds them (kv dtype rounding), appended at position t
+        const KV k0 = from_f<KV>(x0), k1 = from_f<KV>(x1);
+        float* dst = role == NREP ? ks[t] : vs[t];
+        dst[lane] = to_f(k0); dst[lane + half] = to_f(k1);
+        KV* cache = (KV*)(role == NREP ? p.k_cache : p.v_cache) + (((long long)b * nk + h) * p.Lmax + t) * D;
+        cache[lane] = k0; cache[lane + half] = k1;
+      }
+    }
+  }
+  __syncthreads();
+  if (w >= T * NREP) return;
+  const int t = w / NREP, j = w % NREP, r = b * T + t;
+  const float scale = rsqrtf((float)D);
+  const bool act = lane < half;
+  const float q0 = act ? qs[t][j][lane] : 0.f, q1 = act ? qs[t][j][lane + half] : 0.f;
+  float sc[T], mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    float d = act ? q0 * ks[u][lane] + q1 * ks[u][lane + half] : 0.f;
+    d = wave_sum(d) * scale;
+    sc[u] = u <= t ? d : -INFINITY;
+    mx = fmaxf(mx, sc[u]);
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int u = 0; u < T; ++u) { sc[u] = u <= t ? expf(sc[u] - mx) : 0.f; den += sc[u]; }
+  if (!act) return;
+  float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+  for (int u = 0; u < T; ++u) { o0 += sc[u] * vs[u][lane]; o1 += sc[u] * vs[u][lane + half]; }
+  const long long oi = ((long long)r * nq + h * NREP + j) * D;
+  if (p.o_dtype == QT_BF16) {
+    ((bf16_t*)p.out)[oi + lane] = f2bf(o0 / den);
+    ((bf16_t*)p.out)[oi + lane + half] = f2bf(o1 / den);
+  } else {
+    ((float*)p.out)[oi + lane] = o0 / den;
+    ((float*)p.out)[oi + lane + half] = o1 / den;
+  }
+}
+
+template <typename KV, int D>
+int small_prefill_dispatch(const qt_decode_attn_args& a, int T, hipStream_t s) {
+  if (T != 2 || a.R % T) return QT_ERR_SHAPE;
+  dim3 g(a.R / T, a.Hkv);
+  switch (a.Hq / a.Hkv) {
+    case 1: hipLaunchKernelGGL((attn_small_prefill_k<KV, D, 1, 2>), g, dim3(64 * 2 * 3), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((attn_small_prefill_k<KV, D, 2, 2>), g, dim3(64 * 2 * 4), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((attn_small_prefill_k<KV, D, 4, 2>), g, dim3(64 * 2 * 6), 0, s, a); break;
+    default: return QT_ERR_SHAPE;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
 template <typename KV, int D>
 int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
   const int ns = a.nsplit > 1 ? a.nsplit : 1;
@@ -498,6 +584,20 @@ extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
     case 16: return bf ? decode_dispatch<bf16_t, 16>(*a, s) : decode_dispatch<float, 16>(*a, s);
     case 64: return bf ? decode_dispatch<bf16_t, 64>(*a, s) : decode_dispatch<float, 64>(*a, s);
     case 128: return bf ? decode_dispatch<bf16_t, 128>(*a, s) : decode_dispatch<float, 128>(*a, s);
+    default: return QT_ERR_SHAPE;
+  }
+}
+
+extern "C" int qt_small_prefill_attention(const qt_decode_attn_args* a, int T, void* stream) {
+  if (!a || a->R <= 0 || a->Hkv <= 0 || a->Hq % a->Hkv || a->Lmax < T) return QT_ERR_SHAPE;
+  if (a->o_dtype != QT_F32 && a->o_dtype != QT_BF16) return QT_ERR_DTYPE;
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = a->kv_dtype == QT_BF16;
+  if (!bf && a->kv_dtype != QT_F32) return QT_ERR_DTYPE;
+  switch (a->D) {
+    case 16: return bf ? small_prefill_dispatch<bf16_t, 16>(*a, T, s) : small_prefill_dispatch<float, 16>(*a, T, s);
+    case 64: return bf ? small_prefill_dispatch<bf16_t, 64>(*a, T, s) : small_prefill_dispatch<float, 64>(*a, T, s);
+    case 128: return bf ? small_prefill_dispatch<bf16_t, 128>(*a, T, s) : small_prefill_dispatch<float, 128>(*a, T, s);
     default: return QT_ERR_SHAPE;
   }
 }

@@ -75,7 +75,7 @@ class MlpArgs(ctypes.Structure):
 
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
-           "qt_mlp_ws_bytes", "qt_rmsnorm_rec",
+           "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
 
@@ -94,6 +94,7 @@ def load_library(path: str = LIB_PATH):
         "qt_attention": [P, P], "qt_decode_attention": [P, P], "qt_sample": [P, P],
         "qt_rmsnorm": [P, P, c_float, P, c_int, c_int, P],
         "qt_rmsnorm_rec": [P, P, c_float, P, c_int, c_int, P, c_ll, P, c_int, P],
+        "qt_small_prefill_attention": [P, c_int, P],
         "qt_gather_rows": [P, c_int, P, c_int, c_int, P, c_ll, P],
         "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, c_int, P],
         "qt_advance": [P, c_int, P],

@@ -201,6 +201,17 @@ def attention(q, R, Hq, Hkv, D, kc, vc, Lmax, row_batch, row_start, row_len, out
     check(_hip.lib().qt_attention(ctypes.byref(a), stream()), "qt_attention")
 
 
+def small_prefill_attention(qkv, R, T, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc, Lmax, out):
+    """qt_small_prefill_attention: rows b*T + t at positions t < T, keys all new (one launch)."""
+    a = _hip.DecodeAttnArgs()
+    a.R, a.Hq, a.Hkv, a.D, a.Lmax = R, Hq, Hkv, D, Lmax
+    a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    a.k_cache, a.v_cache, a.kv_dtype = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype)
+    a.out, a.o_dtype = ptr(out), _hip.dtype_code(out.dtype)
+    check(_hip.lib().qt_small_prefill_attention(ctypes.byref(a), T, stream()), "qt_small_prefill_attention")
+
+
 def decode_attn_ws_bytes(R, Hq, Hkv, D, nsplit):
     return int(_hip.lib().qt_decode_attn_ws_bytes(R, Hq, Hkv, D, nsplit))
 

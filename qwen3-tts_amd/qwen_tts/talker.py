@@ -73,6 +73,9 @@ class _Stack:
                 K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                    self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
                                    meta["row_start"], kc, vc, Lmax, scratch["att"], const_pos=meta.get("const_pos", -1))
+            elif "small_T" in meta:  # every key is new and rows are [batch][token]: one fused launch
+                K.small_prefill_attention(scratch["qkv"], R, meta["small_T"], self.Hq, self.Hkv, self.D, L.q_norm,
+                                          L.k_norm, self.eps, self.cos, self.sin, kc, vc, Lmax, scratch["att"])
             else:
                 K.qkv_post(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
                            self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
@@ -152,7 +155,7 @@ class Session:
         rb2 = torch.arange(2 * B, device=dev, dtype=torch.int32) // 2
         p2 = torch.arange(2 * B, device=dev, dtype=torch.int32) % 2
         self.cp_meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * B),
-                         "row_batch": rb2}
+                         "row_batch": rb2, "small_T": 2}
         self.cp_meta = []
         for g in range(1, self.G - 1):
             pos = torch.full((B,), g + 1, dtype=torch.int32, device=dev)

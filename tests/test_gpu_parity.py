@@ -357,6 +357,36 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
         torch.testing.assert_close(outs[0], a2, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("D,hq,hkv", [(128, 16, 8), (16, 4, 2), (64, 4, 4)])
+@pytest.mark.parametrize("kvdt", [torch.float32, torch.bfloat16])
+def test_small_prefill_attention_matches_two_kernel_path(D, hq, hkv, kvdt):
+    """Fused 2-token prefill (code-predictor per-frame prefill) == qt_qkv_post + qt_attention."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(D + hq)
+    B, T, Lmax = 5, 2, 18
+    R = B * T
+    qkv = torch.randn(R, (hq + 2 * hkv) * D, generator=g).to(dev)
+    qn, kn = (1 + 0.1 * torch.randn(D, generator=g)).to(dev), (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    cos, sin = Kn.rope_tables(D, 1e6, 64, dev)
+    i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
+    pos = i32([t for _ in range(B) for t in range(T)])
+    rb = i32([b for b in range(B) for _ in range(T)])
+    kc1 = torch.zeros(B, hkv, Lmax, D, device=dev, dtype=kvdt)
+    vc1 = torch.zeros_like(kc1)
+    q = torch.zeros(R, hq * D, device=dev)
+    a1 = torch.zeros(R, hq * D, device=dev)
+    Kn.qkv_post(qkv, R, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, pos, q, kc1, vc1, Lmax)
+    Kn.attention(q, R, hq, hkv, D, kc1, vc1, Lmax, rb, i32([0] * R), pos + 1, a1, T)
+    kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(vc1)
+    a2 = torch.zeros(R, hq * D, device=dev)
+    Kn.small_prefill_attention(qkv, R, T, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc2, vc2, Lmax, a2)
+    ktol = 2e-6 if kvdt == torch.float32 else 1e-2
+    torch.testing.assert_close(kc2.float(), kc1.float(), atol=ktol, rtol=ktol)
+    torch.testing.assert_close(vc2.float(), vc1.float(), atol=0, rtol=0)
+    torch.testing.assert_close(a2, a1, atol=2e-5, rtol=2e-5)
+
+
 def test_sample_greedy_processors():
     from qwen_tts import kernels as Kn
     from oracle.talker import process_logits
