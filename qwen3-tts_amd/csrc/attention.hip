@@ -5,6 +5,7 @@
 // Pass 2: softmax in fp32 over LDS; P.V with the same key-per-lane-group split, reduced across waves.
 // Decode roofline: bytes = 2 * L * D * sizeof(kv) per (row, kv-head) / 8 TB/s.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -195,9 +196,10 @@ int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
 // K and V fragments of IC keys are loaded before any use (IC x 2 KiB in flight per group) and folded
 // into an online softmax; partial (m, l, o) merge across groups by shuffles and across waves via LDS.
 // Bytes per (row, head) = 2 * L * D * sizeof(kv): the decode-attention HBM roofline of SURVEY.md §8(d).
-template <typename KV, int D, int NREP>
-__global__ __launch_bounds__(512) void attn_decode_k(qt_decode_attn_args p) {
-  constexpr int NW = 8;  // waves: 8 x 64 lanes keeps kf/vf/o/q (~150 VGPRs) out of scratch
+template <typename KV, int D, int NREP, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) {
+  // NW waves: 8 for long caches (8 x 64 lanes keeps kf/vf/o/q (~150 VGPRs) out of scratch), 4 for short ones
+  // (code predictor, <= 17 keys: fewer idle waves in the merges)
   constexpr int LPK = D / 8, GPW = 64 / LPK, G = NW * GPW, IC = sizeof(KV) == 2 ? 4 : 2;
   __shared__ float qs[NREP][D];
   __shared__ float knew[D], vnew[D];
@@ -538,10 +540,18 @@ int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
   if (ns > 1 && (!a.ws || a.ws_bytes < qt_decode_attn_ws_bytes(a.R, a.Hq, a.Hkv, a.D, ns))) return QT_ERR_ARG;
   if (ns > 1 && a.R * a.Hkv > 1024) return QT_ERR_SHAPE;  // arrival counters live in the 4 KiB header
   dim3 g(a.R, a.Hkv, ns);
+  static const int nw_env = [] { const char* e = getenv("QT_ATTN_SHORT"); return e ? atoi(e) : -1; }();
+  const bool short_cache = nw_env >= 0 ? nw_env != 0 : a.Lmax <= 64;  // 4 waves cover <= 64 keys in one pass
   switch (a.Hq / a.Hkv) {
-    case 1: hipLaunchKernelGGL((attn_decode_k<KV, D, 1>), g, dim3(512), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((attn_decode_k<KV, D, 2>), g, dim3(512), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4>), g, dim3(512), 0, s, a); break;
+    case 1:
+      if (short_cache) hipLaunchKernelGGL((attn_decode_k<KV, D, 1, 4>), g, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((attn_decode_k<KV, D, 1, 8>), g, dim3(512), 0, s, a);
+      break;
+    case 2:
+      if (short_cache) hipLaunchKernelGGL((attn_decode_k<KV, D, 2, 4>), g, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((attn_decode_k<KV, D, 2, 8>), g, dim3(512), 0, s, a);
+      break;
+    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4, 8>), g, dim3(512), 0, s, a); break;
     default: return QT_ERR_SHAPE;
   }
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;

@@ -353,20 +353,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 constexpr int IG_BM = 128, IG_BN = 64, IG_KC = 32, IG_LDSW = 40;  // LDS row stride 40 bf16 (80 B)
 constexpr int IG_GPT = 3;  // staged 8-channel groups per thread (window rows <= 192)
 
-template <typename AT, typename OT, int NT>
+template <typename AT, typename OT, int NT, int MI>
 __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
+  constexpr int BM = 64 * MI;  // output rows per block (MI 16-row tiles per wave)
   extern __shared__ unsigned char ig_smem[];
   bf16_t* win = (bf16_t*)ig_smem;  // [2][WR][IG_LDSW]
-  __shared__ float ss_row[IG_BM];
+  __shared__ float ss_row[BM];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lm = lane & 15, lk = lane >> 4;
   const bool lin = p.taps == 0;
   const int taps = lin ? 1 : p.taps, dil = lin ? 1 : p.dil;
   const int cin = lin ? p.Klog : p.cin, cin_pad = lin ? p.Kp : p.cin_pad;
   const int t_in = lin ? p.M : p.t_in, t_out = lin ? p.M : p.t_out, t_off = lin ? 0 : p.t_off;
-  const int WR = IG_BM + (taps - 1) * dil;
-  const int tiles_t = (t_out + IG_BM - 1) / IG_BM;
-  const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * IG_BM;
+  const int WR = BM + (taps - 1) * dil;
+  const int tiles_t = (t_out + BM - 1) / BM;
+  const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * BM;
   const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * NT;
   const int nch = cin_pad / IG_KC, ktiles = p.Kp / IG_KC;
   const AT* A = (const AT*)p.A + (long long)bi * t_in * p.lda;
@@ -410,9 +411,9 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
     }
   };
 
-  f32x4_t acc[2][NT];
+  f32x4_t acc[MI][NT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const bf16_t* Wb = (const bf16_t*)p.W + lane * 8;
@@ -437,11 +438,11 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       // one tap ahead: next (tap, chunk) k tile
       const int jn = j + 1 < taps ? j + 1 : 0, cn = j + 1 < taps ? c : c + 1;
       if (cn < nch) load_b(bnxt, jn * nch + cn);
-      u32x4_t af[2];
+      u32x4_t af[MI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const u32x4_t*)(wb + (w * 32 + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
+      for (int i = 0; i < MI; ++i) af[i] = *(const u32x4_t*)(wb + (w * (16 * MI) + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int q = 0; q < NT; ++q)
           acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
@@ -459,13 +460,13 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       const int q = tid + i * 256, r = q >> 2;
-      if ((q & 3) == 0 && r < IG_BM) ss_row[r] = s;
+      if ((q & 3) == 0 && r < BM) ss_row[r] = s;
     }
     __syncthreads();
   }
   OT* out = (OT*)p.out;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
       const int nt = nt0 + q;
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int rl = w * 32 + i * 16 + lk * 4 + e;
+        const int rl = w * (16 * MI) + i * 16 + lk * 4 + e;
         float x = acc[i][q][e];
         if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
         x += bias;
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float up = __shfl_xor(v[e], 8, 64);
-          const int t = t0 + w * 32 + i * 16 + lk * 4 + e;
+          const int t = t0 + w * (16 * MI) + i * 16 + lk * 4 + e;
           if (lm < 8 && t < t_out && nt * 8 + lm < (p.N >> 1))
             out[((long long)bi * t_out + t) * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[e]) * up);
         }
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int t = t0 + w * 32 + i * 16 + lk * 4 + e;
+        const int t = t0 + w * (16 * MI) + i * 16 + lk * 4 + e;
         if (t >= t_out || !nval) continue;
         OT* o = out + ((long long)bi * t_out + t) * p.ldo + n;
         if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[e]);
@@ -595,14 +596,23 @@ int launch(const GemmP& p, hipStream_t s) {
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
     const int taps = p.taps == 0 ? 1 : p.taps, dil = p.taps == 0 ? 1 : p.dil;
     const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;
-    const int WR = IG_BM + (taps - 1) * dil;
-    const size_t smem = (size_t)2 * WR * IG_LDSW * sizeof(bf16_t);
     // column tile per block: 6 x 16 for 96 / 192-channel layers (no idle tiles, the snake-staged window is
-    // shared by all of a row tile's columns), else 8 x 16
-    const int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8;
-    dim3 grid(batches * ((t_out + IG_BM - 1) / IG_BM), (nt + ntb - 1) / ntb);
-    if (ntb == 6) hipLaunchKernelGGL((igemm_k<AT, OT, 6>), grid, dim3(256), smem, s, p);
-    else hipLaunchKernelGGL((igemm_k<AT, OT, 8>), grid, dim3(256), smem, s, p);
+    // shared by all of a row tile's columns), else 8 x 16; QT_IGEMM_CFG = "NT,MI" overrides (measurement)
+    static const int cfg = [] { const char* e = getenv("QT_IGEMM_CFG"); return e ? atoi(e) * 10 + atoi(e + 2) : 0; }();
+    int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8, mi = 2;
+    if (cfg) { ntb = cfg / 10; mi = cfg % 10; }
+    const int bm = 64 * mi;
+    const int WR = bm + (taps - 1) * dil;
+    const size_t smem = (size_t)2 * WR * IG_LDSW * sizeof(bf16_t);
+    dim3 grid(batches * ((t_out + bm - 1) / bm), (nt + ntb - 1) / ntb);
+#define IG_GO(N_, M_) hipLaunchKernelGGL((igemm_k<AT, OT, N_, M_>), grid, dim3(256), smem, s, p)
+    if (ntb == 6 && mi == 2) IG_GO(6, 2);
+    else if (ntb == 6 && mi == 1) IG_GO(6, 1);
+    else if (ntb == 4 && mi == 2) IG_GO(4, 2);
+    else if (ntb == 4 && mi == 1) IG_GO(4, 1);
+    else if (ntb == 8 && mi == 1) IG_GO(8, 1);
+    else IG_GO(8, 2);
+#undef IG_GO
   } else if (p.M <= 32) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 2, 8>), dim3(nt, (p.M + 31) / 32), dim3(512), 0, s, p);
   } else {
