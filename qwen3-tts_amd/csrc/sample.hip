@@ -11,8 +11,7 @@
 
 namespace {
 
-constexpr int NT = 256;
-constexpr int PER = 16;  // V <= 4096
+constexpr int NT = 256;  // threads per row; PER = scores per thread (8 / 12 / 16 for V <= 2048 / 3072 / 4096)
 
 QT_DEV unsigned mulhilo(unsigned a, unsigned b, unsigned* hi) {
   unsigned long long p = (unsigned long long)a * b;
@@ -55,6 +54,7 @@ QT_DEV float block_max(float v, float* sh) {
   return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
 }
 
+template <int PER>
 __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
   __shared__ float sh[8];
   __shared__ int shi[4];
@@ -176,6 +176,7 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
       }
       int P2 = 1;
       while (P2 < V) P2 <<= 1;
+      for (int v = PER * NT + tid; v < P2; v += NT) srt[v] = -INFINITY;  // slots beyond this PER's reach
       __syncthreads();
       for (int k = 2; k <= P2; k <<= 1)
         for (int jj = k >> 1; jj > 0; jj >>= 1) {
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
     float e[PER], mass = 0.f;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      e[j] = (tid + j * NT < V && okey(s[j]) >= tk && s[j] > -INFINITY) ? expf(s[j] - mx) : 0.f;
+      e[j] = (tid + j * NT < V && okey(s[j]) >= tk && s[j] > -INFINITY) ? __expf(s[j] - mx) : 0.f;
       mass += e[j];
     }
     // inclusive prefix of per-thread masses (wave scan + wave offsets)
@@ -265,9 +266,12 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
 }  // namespace
 
 extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
-  if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * PER || !a->tok_out) return QT_ERR_SHAPE;
+  if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * 16 || !a->tok_out) return QT_ERR_SHAPE;
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
-  hipLaunchKernelGGL(sample_k, dim3(a->R), dim3(NT), 0, (hipStream_t)stream, *a);
+  hipStream_t st = (hipStream_t)stream;
+  if (a->V <= NT * 8) hipLaunchKernelGGL(sample_k<8>, dim3(a->R), dim3(NT), 0, st, *a);
+  else if (a->V <= NT * 12) hipLaunchKernelGGL(sample_k<12>, dim3(a->R), dim3(NT), 0, st, *a);
+  else hipLaunchKernelGGL(sample_k<16>, dim3(a->R), dim3(NT), 0, st, *a);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }

@@ -473,6 +473,25 @@ def test_sample_top_p_support():
     assert abs((t == 0).float().mean().item() - 0.4 / 0.7) < 0.06
 
 
+@pytest.mark.parametrize("V", [2048, 3072, 4096])
+def test_sample_top_p_large_vocab(V):
+    """TopP on full-size vocabularies (every per-thread register width): draws stay inside the nucleus."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    R = 256
+    g = torch.Generator().manual_seed(V)
+    logits = torch.randn(R, V, generator=g) * 3
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=0, top_p=0.8, temperature=1.0, seed=4,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    p = torch.softmax(logits, -1)
+    sp, idx = p.sort(-1, descending=True)
+    keep = (sp.cumsum(-1) - sp) < 0.8  # TopPLogitsWarper: smallest prefix reaching top_p
+    t = tok.cpu().long()
+    for r in range(R):
+        assert int(t[r]) in set(idx[r][keep[r]].tolist())
+
+
 # ------------------------------------------------------------------------------------------ end-to-end talker
 @pytest.fixture(scope="module")
 def tiny_models():
