@@ -673,9 +673,10 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   if (a->M <= 16 && a->taps == 0 && a->K % KT == 0 && a->gamma == nullptr && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN &&
       a->splitk != 1 && ntl <= 4096) {
     // auto: split only deep-K shapes on < 256 column tiles (measured: the ~2 us arrival/reduce cost pays
-    // only when it removes a second weight round trip, e.g. down-proj 2048x6144 12.4 -> 10.7 us)
+    // only when it removes a second weight round trip; down-proj with bf16 activations: 2048x6144 10.1 ->
+    // 9.8 us, 1024x3072 7.4 -> 7.1 us at split 2, split 4 slower)
     const int wpb1 = ktl >= 48 ? 16 : (ktl >= 16 ? 8 : 4), per1 = (ktl + wpb1 - 1) / wpb1;
-    int ks = a->splitk > 1 ? a->splitk : ((per1 > 4 && ntl < 256) ? (ntl >= 128 ? 2 : 4) : 1);
+    int ks = a->splitk > 1 ? a->splitk : ((per1 > 4 && ntl < 256) ? 2 : 1);  // bf16-A down-proj: 2 best
     ks = std::max(1, std::min({ks, 16, ktl / 2}));
     const size_t need = 4096 * sizeof(unsigned) + (size_t)ntl * ks * (64 * 4 + 16) * sizeof(float);
     if (ks > 1 && need <= (size_t)a->ws_bytes) {

@@ -58,6 +58,20 @@ def main():
                 if not rms:
                     print(f"{'':60s} -> {Nn * Kk * 2 / us / 1e3:8.1f} GB/s")
         del Ws
+    # bf16 activations (attention / SwiGLU outputs feeding o-proj / down-proj in bf16 mode), residual add
+    for (Nn, Kk) in [(1024, 3072), (1024, 2048), (2048, 6144), (2048, 2048)]:
+        nmat = max(2, int(600e6 // (Nn * Kk * 2)))
+        Ws = [K.tile_linear(torch.randn(Nn, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
+        A = torch.randn(8, Kk, device=dev).bfloat16()
+        out = torch.zeros(8, Nn, device=dev)
+        for sk in (1, 2, 4, 8, 0):
+            it = {"i": 0}
+
+            def f():
+                K.gemm(A, Ws[it["i"] % nmat], out, 8, Kk, Nn, splitk=sk, epi=_hip.EPI_ADD)
+                it["i"] += 1
+            timed(f, f"COLD gemv bf16-A add M=8 N={Nn} K={Kk} splitk={sk}")
+        del Ws
     lg = torch.randn(8, 3072, device=dev)
     tok = torch.zeros(8, dtype=torch.int32, device=dev)
     step = torch.zeros(1, dtype=torch.int32, device=dev)
