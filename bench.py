@@ -140,12 +140,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test-only overrides: rehearse the N>1 path on one GPU (all ranks on cuda:0, gloo collectives)
+    backend = os.environ.get("QT_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
+    if os.environ.get("QT_BENCH_SAME_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from qwen_tts import Qwen3TTSModel
     cfg, W, CW = make_weights(a.preset, dev, world, rank)

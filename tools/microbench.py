@@ -58,6 +58,21 @@ def main():
                 if not rms:
                     print(f"{'':60s} -> {Nn * Kk * 2 / us / 1e3:8.1f} GB/s")
         del Ws
+    # rms GEMVs reading the residual stream as fp32 vs bf16 (gate/up + SwiGLU epilogue, qkv)
+    for (Nn, Kk, epi) in [(12288, 2048, _hip.EPI_SWIGLU), (4096, 2048, _hip.EPI_STORE), (6144, 1024, _hip.EPI_SWIGLU),
+                          (4096, 1024, _hip.EPI_STORE)]:
+        nmat = max(2, int(600e6 // (Nn * Kk * 2)))
+        Ws = [K.tile_linear(torch.randn(Nn, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
+        for adt in (torch.float32, torch.bfloat16):
+            A = torch.randn(8, Kk, device=dev).to(adt)
+            out = torch.zeros(8, Nn, device=dev, dtype=torch.bfloat16)
+            it = {"i": 0}
+
+            def f():
+                K.gemm(A, Ws[it["i"] % nmat], out, 8, Kk, Nn, rms=True, eps=1e-6, epi=epi)
+                it["i"] += 1
+            timed(f, f"COLD gemv rms A={str(adt)[6:]} M=8 N={Nn} K={Kk}")
+        del Ws
     # bf16 activations (attention / SwiGLU outputs feeding o-proj / down-proj in bf16 mode), residual add
     for (Nn, Kk) in [(1024, 3072), (1024, 2048), (2048, 6144), (2048, 2048)]:
         nmat = max(2, int(600e6 // (Nn * Kk * 2)))
