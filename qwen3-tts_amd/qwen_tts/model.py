@@ -159,35 +159,38 @@ class TTSModel:
         return self.engine.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=use_graph)
 
     # -------------------------------------------------------------------------------- streaming
+    REF_CHUNK, REF_CTX = 300, 25  # Qwen3TTSTokenizerV2Decoder.chunked_decode (K:885-895)
+
     @torch.no_grad()
     def stream(self, input_ids=None, instruct_ids=None, ref_ids=None, voice_clone_prompt=None, languages=None,
                speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=0,
-               first_chunk_frames=12, chunk_frames=48, left_context=25, use_graph=True, **kwargs):
+               first_chunk_frames=12, chunk_frames=48, left_context=325, use_graph=True, **kwargs):
         """Streaming generation (the reference has none): yields (row, pcm, last) as frames finish.
 
-        pcm is a 1-D fp32 device tensor of 24 kHz samples; per row the chunks concatenate to exactly the length of
-        the one-shot batch decode (Z:259-365 right-pads shorter rows with code-0 frames: a row shorter than the
-        batch keeps 1920 F samples, the longest rows 1920 F - 555; the cap at 1920 x #nonzero cb0 is applied to
-        the last chunk, so a row whose codebook 0 contains code 0 mid-stream can stream more than it keeps).  Chunk [s, e) is
-        decoded from codes [s - ctx, e + 1): ctx = min(left_context, s) frames of left context -- the context
-        the reference's own chunked decode uses (K:885-895) -- and one lookahead frame for the transposed
-        convs, keeping samples [1920 s, 1920 e); a row's last chunk is decoded to its end.  Codes are
-        identical to generate(); with left_context >= F the PCM equals the one-shot decode up to fp rounding."""
+        Per row the chunks concatenate to the one-shot generate() + decode() PCM (Z:259-365): the reference
+        decodes the zero-right-padded batch in 300-frame chunks with 25 frames of left context, dropping the
+        last 555 samples of each chunk (no next frame), and keeps 1920 x #nonzero-cb0 samples.  A streamed
+        window [s, e) never crosses a chunk boundary and is decoded from its chunk's start (minus those 25
+        context frames) plus one lookahead frame, so it reproduces that output up to fp rounding.
+        `left_context` < 325 caps the re-decoded history per window (less work, approximate: in fp32 150 frames
+        -> rel-L2 1e-6, 72 -> 7e-4, 25 -> 2e-2; tools/stream_fidelity.py).  Codes are identical to generate().
+        pcm is a 1-D fp32 device tensor of 24 kHz samples."""
         dec = self.speech_tokenizer.model
         up = dec.total_upsample
+        RC, RX = self.REF_CHUNK, self.REF_CTX
         emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
                                                    voice_clone_prompt, ref_ids)
         gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
                        subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
         eos = self.engine.tc["codec_eos_token_id"]
         B = emb.shape[0]
-        emitted = 0                       # frames [0, emitted) emitted for every unfinished row
-        end = [None] * B                  # EOS frame per row once seen
+        emitted = 0                       # windows [0, emitted) decoded for every row
+        end = [None] * B                  # frame count of each row once its EOS is seen
+        cap = [None] * B                  # one-shot sample count (1920 x #nonzero cb0) once the row has ended
         done = [False] * B
         cum = [0] * B                     # samples emitted per row
-        nonzero = [0] * B                 # #nonzero cb0 among the row's frames (length cap)
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames + 1)
         for sessions, frames, final in it:
@@ -199,38 +202,41 @@ class TTSModel:
                     hit = (c0[b, emitted:] == eos).nonzero()
                     if hit.numel():
                         end[b] = emitted + int(hit[0])
-            stop = frames if final else frames - 1  # rows that continue keep frame `frames-1` as lookahead
-            if frames <= emitted:
-                if not final:
-                    continue
-            ctx = left_context if emitted - left_context > 0 else emitted
-            w = None
-            if frames > emitted:
-                cc = codes[:, emitted - ctx:frames].clone()
-                for b in range(B):  # a finished row continues as the one-shot batch decode's zero padding
-                    if end[b] is not None and end[b] < frames:
+                if final and end[b] is None:
+                    end[b] = frames
+                if end[b] is not None and cap[b] is None:
+                    cap[b] = up * int((c0[b, :end[b]] != 0).sum())
+            # the batch's length once known: every row ended (longest row), or generation stopped
+            t_end = max(end) if all(x is not None for x in end) else None
+            target = t_end if t_end is not None else frames - 1  # else keep frame `frames-1` as lookahead
+            while emitted < target:
+                k = emitted // RC
+                cend = (k + 1) * RC
+                e = min(target, cend)
+                closed = e == cend or e == t_end  # this reference chunk ends at e
+                base = k * RC - (RX if k * RC - RX > 0 else k * RC)
+                ctx = min(emitted - base, left_context)
+                hi = e if closed else e + 1
+                cc = codes[:, emitted - ctx:hi].clone()
+                for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
+                    if end[b] is not None and end[b] < hi:
                         cc[b, max(end[b] - (emitted - ctx), 0):] = 0
                 w = dec.forward(cc)
-            fmax = max(e if e is not None else frames for e in end) if final else None
-            for b in range(B):
-                if done[b]:
-                    continue
-                last = final or (end[b] is not None and end[b] <= frames)
-                e_b = (end[b] if end[b] is not None else frames) if last else stop
-                n = e_b - emitted
-                take = 0
-                if n > 0 and w is not None:
-                    nonzero[b] += int((c0[b, emitted:e_b] != 0).sum())
-                    # only the batch's longest rows lose the final 555 samples (no next frame); shorter rows see
-                    # the zero padding frame as lookahead, exactly like the padded one-shot decode
-                    take = up * n - (555 if last and final and e_b == fmax else 0)
-                    if last:  # one-shot length cap (Z:259-365 counts nonzero cb0; only binds if cb0 == 0 occurs)
-                        take = min(take, up * nonzero[b] - cum[b])
-                    take = max(0, take)
-                chunk = w[b, ctx * up:ctx * up + take] if take > 0 else torch.zeros(0, device=codes.device)
-                cum[b] += take
-                done[b] = last
-                yield b, chunk, last
-            emitted = stop
+                n = up * (e - emitted) - (555 if closed else 0)
+                for b in range(B):
+                    if done[b]:
+                        continue
+                    take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
+                    chunk = w[b, ctx * up:ctx * up + take]
+                    cum[b] += take
+                    last = cap[b] is not None and (cum[b] >= cap[b] or e == t_end)
+                    done[b] = last
+                    yield b, chunk, last
+                emitted = e
+            if t_end is not None and emitted >= t_end:
+                for b in range(B):  # rows whose output was complete before the last window
+                    if not done[b]:
+                        done[b] = True
+                        yield b, torch.zeros(0, device=codes.device), True
             if all(done):
                 break

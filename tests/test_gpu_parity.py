@@ -569,11 +569,11 @@ def test_row_groups_identical_to_whole_batch(tiny_models, dtype):
             np.testing.assert_array_equal(a.numpy(), b.numpy())
 
 
-@pytest.mark.parametrize("ctx,eos", [(1000, False), (1000, True), (2, True)])
-def test_stream_matches_one_shot(tiny_models, ctx, eos):
+@pytest.mark.parametrize("ctx,eos,frames", [(1000, False, 30), (1000, True, 24), (2, True, 24), (1000, False, 331)])
+def test_stream_matches_one_shot(tiny_models, ctx, eos, frames):
     """stream(): per utterance the PCM chunks concatenate to exactly the one-shot generate+decode length
-    (EOS-ragged batch included); with left context covering the utterance they equal the one-shot PCM; the
-    first chunk (no left context needed) always does."""
+    (EOS-ragged batch and > 300-frame chunk restarts included); with left context covering each reference
+    chunk they equal the one-shot PCM; the first chunk (no left context needed) always does."""
     from cases import gen_kwargs, make_inputs, talker_cases
     from oracle import codec_param_specs, load_preset, synth_state_dict
     from qwen_tts import Qwen3TTSTokenizer
@@ -592,7 +592,7 @@ def test_stream_matches_one_shot(tiny_models, ctx, eos):
     tok = Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer", dtype="fp32", weights=CW)
     model.load_speech_tokenizer(tok)
     key = "cv_b2_stream_dialect"
-    case = dict(talker_cases()[key], max_new_tokens=24 if eos else 30)
+    case = dict(talker_cases()[key], max_new_tokens=frames)
     ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
     kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=case["languages"],
               speakers=case["speakers"], non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
