@@ -18,7 +18,7 @@ import torch
 
 from ..model import TTSModel
 from ..text import load_processor
-from ..weights import load_safetensors, read_json, resolve_path, synthetic, talker_specs
+from ..weights import is_preset_dir, load_safetensors, read_json, resolve_path, synthetic, talker_specs
 from .qwen3_tts_tokenizer import Qwen3TTSTokenizer, _dtype_name
 
 AudioLike = Union[str, np.ndarray, Tuple[np.ndarray, int]]
@@ -58,6 +58,8 @@ class Qwen3TTSModel:
         dev = torch.device(device_map if isinstance(device_map, str) and device_map.startswith("cuda") else "cuda:0")
         W = weights if weights is not None else load_safetensors(d)
         if not W:
+            if not is_preset_dir(d):
+                raise FileNotFoundError(f"no model*.safetensors in checkpoint directory {d!r}")
             W = synthetic(talker_specs(cfg), dev, seed)
         with torch.cuda.device(dev):
             m = TTSModel(cfg, W, dtype=_dtype_name(dtype), device=dev, generate_config=gen)

@@ -15,7 +15,7 @@ import torch
 from torch.nn.utils.rnn import pad_sequence
 
 from ..codec import CodecDecoder
-from ..weights import codec_specs, load_safetensors, read_json, resolve_path, synthetic
+from ..weights import codec_specs, is_preset_dir, load_safetensors, read_json, resolve_path, synthetic
 
 
 def _dtype_name(dtype) -> str:
@@ -47,6 +47,8 @@ class Qwen3TTSTokenizer:
         dev = torch.device(device_map if isinstance(device_map, str) and device_map.startswith("cuda") else "cuda:0")
         W = weights if weights is not None else load_safetensors(d)
         if not W:
+            if not is_preset_dir(d):
+                raise FileNotFoundError(f"no model*.safetensors in tokenizer directory {d!r}")
             W = synthetic(codec_specs(ccfg), dev, seed)
         inst.config = ccfg
         inst.device = dev

@@ -44,6 +44,11 @@ def resolve_path(name_or_path: str) -> str:
     raise FileNotFoundError(f"no checkpoint directory or preset for {name_or_path!r}")
 
 
+def is_preset_dir(d: str) -> bool:
+    """True for the packaged synthetic-weight presets (the only directories allowed to have no weights)."""
+    return os.path.abspath(d).startswith(os.path.abspath(PRESETS) + os.sep)
+
+
 def read_json(path):
     with open(path) as f:
         return json.load(f)

@@ -531,6 +531,41 @@ def test_talker_greedy_codes_bit_exact(tiny_models, use_graph):
             np.testing.assert_allclose(hid[j].numpy(), z[f"{key}/hidden{j}"], atol=2e-4, rtol=2e-4, err_msg=key)
 
 
+def test_checkpoint_directory_drop_in(tiny_models, tmp_path):
+    """A checkpoint directory in the reference's on-disk layout (config.json, generation_config.json,
+    model.safetensors keyed by the reference state_dict names, speech_tokenizer/{config.json,
+    model.safetensors}) loads through Qwen3TTSModel.from_pretrained and reproduces the golden codes; a
+    directory without weights is an error (no silent synthetic fallback outside the packaged presets)."""
+    import shutil
+    from safetensors.torch import save_file
+    from cases import talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSModel
+    from qwen_tts.weights import resolve_path
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    src = resolve_path("synthetic:tiny-customvoice")
+    for f in ("config.json", "generation_config.json"):
+        shutil.copy(os.path.join(src, f), tmp_path / f)
+    save_file({k: v.contiguous() for k, v in W.items()}, str(tmp_path / "model.safetensors"))
+    (tmp_path / "speech_tokenizer").mkdir()
+    shutil.copy(os.path.join(src, "speech_tokenizer", "config.json"), tmp_path / "speech_tokenizer" / "config.json")
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    save_file(CW, str(tmp_path / "speech_tokenizer" / "model.safetensors"))
+    tts = Qwen3TTSModel.from_pretrained(str(tmp_path), dtype=torch.float32)
+    z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+    cases = talker_cases()
+    key = "cv_b2_stream_dialect"
+    codes, _ = _run_case(tts.model, key, cases[key], list(cases).index(key), cfg)
+    for j, c in enumerate(codes):
+        np.testing.assert_array_equal(c.numpy(), z[f"{key}/codes{j}"])
+    wavs, sr = tts.model.speech_tokenizer.decode([{"audio_codes": c} for c in codes])
+    assert sr == 24000 and all(w.shape[0] > 0 for w in wavs)
+    (tmp_path / "model.safetensors").unlink()
+    with pytest.raises(FileNotFoundError):
+        Qwen3TTSModel.from_pretrained(str(tmp_path), dtype=torch.float32)
+
+
 def test_talker_eos_ragged_bit_exact(tiny_models):
     from cases import talker_cases
     from qwen_tts.model import TTSModel
