@@ -31,6 +31,7 @@ struct GemmP {
   int ks;                       // split-K factor (gridDim.y), 1 = none
   int wpb_max;                  // waves-per-block cap of the decode GEMV (16, or 8 for wide grids)
   int no_igemm;                 // 1: keep large-M GEMMs on gemm_wt (A/B measurement)
+  int ntl;                      // 1: non-temporal weight loads (decode GEMV over >= 16 MiB of weights)
   unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
   const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
 };
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
 // by select, so every chunk issues its U weight fragments (1 KiB contiguous per wave-instruction), A
 // fragments and gamma before a single wait -- the block keeps all of its weight bytes in flight.
 // Split-K partials reduce through LDS; the epilogue is shared with gemm_wt.
-template <typename WT, typename AT, typename OT, int WPB, int U, bool NORM>
+template <typename WT, typename AT, typename OT, int WPB, int U, bool NORM, bool NTL>
 __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   constexpr bool BF = sizeof(WT) == 2;
   constexpr int E = BF ? 8 : 4;
@@ -234,7 +235,10 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kc = min(c + u, kt1 - 1);
-      wv[u] = *(const u32x4_t*)(wp + (size_t)kc * 64 * E);
+      if constexpr (NTL)  // streamed-once weights: non-temporal, so they do not evict re-read data from L2 / MALL
+        wv[u] = __builtin_nontemporal_load((const u32x4_t*)(wp + (size_t)kc * 64 * E));
+      else
+        wv[u] = *(const u32x4_t*)(wp + (size_t)kc * 64 * E);
       if constexpr (E == 8) load8f(arow + kc * KT, a[u]); else load4f(arow + kc * KT, a[u]);
     }
 #pragma unroll
@@ -563,8 +567,14 @@ __global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
 
 template <typename WT, typename AT, typename OT, int WPB, int U>
 void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
-  if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
-  else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false>), dim3(nt, p.ks), dim3(WPB * 64), 0, s, p);
+  const dim3 grid(nt, p.ks), block(WPB * 64);
+  if (p.ntl) {
+    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, true>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, true>), grid, block, 0, s, p);
+  } else {
+    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, false>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, false>), grid, block, 0, s, p);
+  }
 }
 
 // U = k tiles in flight per wave: 8 when a wave owns 5..8 (one round trip instead of two; measured slower at 12)
@@ -662,6 +672,11 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   if ((p.sn_a == nullptr) != (p.sn_ib == nullptr)) return QT_ERR_ARG;
   static const int no_ig = [] { const char* e = getenv("QT_NO_IGEMM"); return e ? atoi(e) : 0; }();
   p.no_igemm = no_ig;
+  // weights streamed once per frame (talker-size matrices) bypass cache retention so the re-read code-predictor
+  // weights stay in L2 / Infinity Cache; QT_GEMV_NT=0/1 forces it off/on for every decode GEMV (measurement)
+  static const int nt_env = [] { const char* e = getenv("QT_GEMV_NT"); return e ? atoi(e) : -1; }();
+  const long long wbytes = (long long)((a->N + 15) / 16) * 16 * p.Kp * (a->w_dtype == QT_BF16 ? 2 : 4);
+  p.ntl = nt_env >= 0 ? nt_env : (wbytes >= (16ll << 20));
   // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
   p.ks = 1; p.cnt = nullptr; p.part = nullptr;
   // wide grids use smaller blocks so several fit per CU (fewer block rounds; measured: N=12288 K=2048
