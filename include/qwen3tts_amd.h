@@ -21,7 +21,10 @@ extern "C" {
 #endif
 
 enum { QT_F32 = 0, QT_BF16 = 1 };
-enum { QT_ACT_NONE = 0, QT_ACT_SILU = 1, QT_ACT_GELU = 2 };
+enum { QT_ACT_NONE = 0, QT_ACT_SILU = 1, QT_ACT_GELU = 2, QT_ACT_RELU = 3, QT_ACT_SIGMOID = 4,
+       QT_ACT_RELU_TANH = 5 /* tanh(relu(x)): ECAPA attentive pooling M:232 */ };
+enum { QT_AACT_NONE = 0, QT_AACT_ELU = 1 };  /* activation applied to the A operand as it is loaded */
+enum { QT_PAD_ZERO = 0, QT_PAD_REFLECT = 1, QT_PAD_REPLICATE = 2 };
 enum { QT_EPI_STORE = 0, QT_EPI_ADD = 1, QT_EPI_SWIGLU = 2 };
 enum { QT_OK = 0, QT_ERR_ARG = -1, QT_ERR_SHAPE = -2, QT_ERR_DTYPE = -3, QT_ERR_LAUNCH = -4 };
 
@@ -67,6 +70,9 @@ typedef struct qt_gemm_args {
   /* optional SnakeBeta on the A operand (K:577-615), per input channel: a' = a + inv_beta[c]*sin(alpha[c]*a)^2
    * (alpha / inv_beta pre-exponentiated); fuses the activation that precedes every codec conv */
   const float* snake_alpha; const float* snake_inv_beta;
+  /* QT_AACT_ELU: ELU(alpha = 1) on every A element (zero padding stays zero) -- the nn.ELU that precedes every
+   * MimiConv1d of the tokenizer encoder (transformers modeling_mimi.py MimiEncoder / MimiResnetBlock) */
+  int a_act;
 } qt_gemm_args;
 #define QT_GEMM_WS_MIN (4 << 20)
 
@@ -214,6 +220,44 @@ int qt_dwconv_ln(const void* x, int dtype, int B, int T, int C, const float* w, 
                  const float* ln_b, float eps, void* out, void* stream);
 /* clamp(-1, 1) + dtype -> fp32 pcm (K:883). */
 int qt_clamp_pcm(const void* x, int dtype, long long n, float* out, void* stream);
+
+/* ---- voice-clone front end ----
+ * T = transformers models/mimi/modeling_mimi.py (the tokenizer encoder, K:898-907, 960-990);
+ * M:95-470, 1940-1954 = mel spectrogram + ECAPA-TDNN speaker encoder. */
+/* Time-axis pad / copy, channels-last: out[b][t][c] (t < t_total) = src(x)[b][t - left][c] (+ x2 likewise),
+ * src per mode for t - left outside [0, T): QT_PAD_ZERO -> 0, QT_PAD_REFLECT -> mirrored (torch "reflect"),
+ * QT_PAD_REPLICATE -> edge row; rows >= T + left + right are zero.  Replaces the F.pad of MimiConv1d (T:327-347),
+ * Conv1d(padding="same", padding_mode="reflect") (M:246-266) and mel_spectrogram's reflect pad (M:446-449);
+ * x2 = the Res2Net running sum (M:114-119).  Strides are in elements (row = one time step). */
+int qt_pad_time(const void* x, long long ldx, const void* x2, long long ldx2, int dtype, int B, int T, int C, int left,
+                int right, int mode, int t_total, void* out, long long ldo, void* stream);
+/* x[b][t][0..C) = 0 for v <= t < Tp (batch stride Tp*ldx): the right "extra" zero padding of a strided MimiConv1d
+ * (T:269-279) when the buffer is longer than the valid length. */
+int qt_zero_tail(void* x, int dtype, int B, int Tp, int v, int C, long long ldx, void* stream);
+/* nn.LayerNorm (T:735-736): out = (x - mean) * rsqrt(var + eps) * w + b per row; x fp32, out dtype. */
+int qt_layernorm(const float* x, long long ldx, const float* w, const float* b, float eps, void* out, int o_dtype,
+                 long long ldo, int M, int N, void* stream);
+/* Residual VQ encode (MimiResidualVectorQuantizer.encode T:1050-1068 / MimiEuclideanCodebook.quantize T:985-991):
+ * per row r: res = x[r]; for q < Q: code = argmin_c |res - E_q[c]|^2 (lowest index on ties), res -= E_q[code];
+ * codes[r*codes_ld + q] = code.  tab [Q][cb][D] (embed_sum / clamp(cluster_usage, 1e-5)), tabT = the same
+ * transposed [Q][D][cb].  D <= 1024, cb % 64 == 0. */
+int qt_rvq_encode(const float* x, long long ldx, const float* tab, const float* tabT, int Q, int cb, int D, int R,
+                  int* codes, long long codes_ld, void* stream);
+/* log-mel from a real DFT (M:451-468): spec [F][ld_spec] holds (re, im) pairs of nbin bins;
+ * out[f][m] = log(max(sum_k basis[m][k] * sqrt(re^2 + im^2 + 1e-9), 1e-5)). */
+int qt_mel_logmag(const float* spec, long long ld_spec, int F, int nbin, const float* basis, int nmel, float* out,
+                  long long ldo, void* stream);
+/* Per-(item, channel) statistics over time (AttentiveStatisticsPooling._compute_statistics M:204-207,
+ * SqueezeExcitationBlock mean M:146): w = softmax_t(logits[b][t][c]) (logits != NULL) or 1/T;
+ * mean = sum_t w x, std = sqrt(max(sum_t w (x - mean)^2, eps)); mean/std at out[b*ld_out + c] (std optional). */
+int qt_time_stats(const void* x, int dtype, long long ldx, const float* logits, long long ldl, int B, int T, int C,
+                  float eps, float* mean_out, float* std_out, long long ld_out, void* stream);
+/* out[b][t][c] = x[b][t][c] * s[b*lds + c] + res[b][t][c] (SE excitation + block residual, M:150, 322). */
+int qt_scale_add(const void* x, long long ldx, const float* s, long long lds, const void* res, long long ldr, int dtype,
+                 int B, int T, int C, void* out, long long ldo, void* stream);
+/* out[b][t][0..W) = v[b*ldv + 0..W) for all t < T (the mean / std broadcast of attentive pooling, M:225-227). */
+int qt_bcast_rows(const float* v, long long ldv, int B, int T, int W, void* out, int o_dtype, long long ldo,
+                  void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,10 +32,22 @@ def synth_param(name: str, shape, seed: int = 1234) -> np.ndarray:
     shape = tuple(int(s) for s in shape)
     g = _rng(seed, name)
     n = lambda: g.standard_normal(shape, dtype=np.float32)  # noqa: E731
-    if name.endswith("_codebook.cluster_usage"):
+    if name.endswith("_codebook.cluster_usage") or name.endswith(".codebook.cluster_usage"):
         return g.uniform(0.5, 2.0, shape).astype(np.float32)
-    if name.endswith("_codebook.embedding_sum"):
+    if name.endswith("_codebook.embedding_sum") or name.endswith(".codebook.embed_sum"):
         return n()
+    if name.endswith(".codebook.initialized"):
+        return np.ones(shape, np.float32)
+    if (name.startswith("encoder.") or name.startswith("speaker_encoder.")) and name.endswith("weight") \
+            and len(shape) in (2, 3) and "norm" not in name:
+        # tokenizer encoder (Mimi) / ECAPA convs and linears: fan-in scaled so activations stay O(1)
+        fan_in = shape[1] * (shape[2] if len(shape) == 3 else 1)
+        gain = 1.0
+        if name.startswith("speaker_encoder."):
+            gain = 1.4  # ReLU
+        elif name.endswith("block.3.conv.weight"):
+            gain = 0.5  # resnet-block output onto the residual stream
+        return (gain * n() / np.sqrt(fan_in)).astype(np.float32)
     if name.endswith(".alpha") or name.endswith(".beta"):  # SnakeBeta (log-scale params)
         return (0.1 * n()).astype(np.float32)
     if name.endswith("layer_scale.scale") or name.endswith(".gamma"):

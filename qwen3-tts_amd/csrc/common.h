@@ -69,6 +69,18 @@ QT_DEV float group_sum_dpp(float v) {
 
 QT_DEV float silu_f(float g) { return g / (1.0f + expf(-g)); }
 QT_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+QT_DEV float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+// GEMM epilogue activation (QT_ACT_*)
+QT_DEV float act_f(float x, int act) {
+  switch (act) {
+    case QT_ACT_SILU: return silu_f(x);
+    case QT_ACT_GELU: return gelu_f(x);
+    case QT_ACT_RELU: return fmaxf(x, 0.f);
+    case QT_ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+    case QT_ACT_RELU_TANH: return tanhf(fmaxf(x, 0.f));
+    default: return x;
+  }
+}
 
 // 8 consecutive elements -> fp32 (16 B of bf16 or 32 B of fp32)
 QT_DEV void load8f(const float* p, float* o) {

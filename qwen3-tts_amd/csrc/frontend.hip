@@ -1,0 +1,323 @@
+// Voice-clone front end kernels: the non-GEMM pieces of the 12 Hz tokenizer ENCODER
+// (Mimi: padding, LayerNorm, residual-VQ nearest-codeword search) and of the mel + ECAPA-TDNN speaker encoder
+// (reflect padding, log-mel, time statistics / attentive pooling, squeeze-excitation).  Every conv / linear of
+// both networks runs on the weight-tiled MFMA GEMM (gemm.hip); these kernels are the glue between them.
+// All of it is bandwidth- or latency-bound one-shot work per reference clip (a 3 s clip is 38 frames).
+//
+// T = transformers models/mimi/modeling_mimi.py, M = qwen_tts/core/models/modeling_qwen3_tts.py.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------------------
+// time-axis pad / copy (channels-last); one thread per output element, channels fastest (coalesced)
+template <typename T>
+__global__ void pad_time_k(const T* __restrict__ x, long long ldx, const T* __restrict__ x2, long long ldx2, int B,
+                           int Tn, int C, int left, int right, int mode, int t_total, T* __restrict__ out, long long ldo) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tot = (long long)B * t_total * C;
+  if (idx >= tot) return;
+  const int c = (int)(idx % C);
+  const long long bt = idx / C;
+  const int t = (int)(bt % t_total), b = (int)(bt / t_total);
+  int s = t - left;
+  float v = 0.f;
+  bool ok = t < Tn + left + right;
+  if (ok && (s < 0 || s >= Tn)) {
+    if (mode == QT_PAD_REFLECT) s = s < 0 ? -s : 2 * (Tn - 1) - s;
+    else if (mode == QT_PAD_REPLICATE) s = s < 0 ? 0 : Tn - 1;
+    else ok = false;
+  }
+  if (ok) {
+    v = to_f(x[((long long)b * Tn + s) * ldx + c]);
+    if (x2) v += to_f(x2[((long long)b * Tn + s) * ldx2 + c]);
+  }
+  out[((long long)b * t_total + t) * ldo + c] = from_f<T>(v);
+}
+
+template <typename T>
+__global__ void zero_tail_k(T* __restrict__ x, int B, int Tp, int v, int C, long long ldx) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int rows = Tp - v;
+  if (idx >= (long long)B * rows * C) return;
+  const int c = (int)(idx % C);
+  const long long br = idx / C;
+  const int t = v + (int)(br % rows), b = (int)(br / rows);
+  x[((long long)b * Tp + t) * ldx + c] = from_f<T>(0.f);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// LayerNorm: one 256-thread block per row, two passes over the row (mean, then centred variance) like torch
+template <typename OT>
+__global__ __launch_bounds__(256) void layernorm_k(const float* __restrict__ x, long long ldx, const float* __restrict__ w,
+                                                   const float* __restrict__ b, float eps, OT* __restrict__ out,
+                                                   long long ldo, int N) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* xr = x + (long long)row * ldx;
+  auto block_sum = [&](float s) {
+    s = wave_sum(s);
+    __syncthreads();
+    if (lane == 0) red[wv] = s;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  float s = 0.f;
+  for (int i = tid; i < N; i += 256) s += xr[i];
+  const float mean = block_sum(s) / (float)N;
+  float q = 0.f;
+  for (int i = tid; i < N; i += 256) { const float d = xr[i] - mean; q += d * d; }
+  const float rs = rsqrtf(block_sum(q) / (float)N + eps);
+  OT* o = out + (long long)row * ldo;
+  for (int i = tid; i < N; i += 256) o[i] = from_f<OT>((xr[i] - mean) * rs * w[i] + b[i]);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Residual VQ encode.  One 256-thread block per frame row; the residual lives in LDS.  For each codebook the
+// block scores all cb codewords (thread t owns codewords t, t+256, ...; the transposed table makes each d-step
+// one coalesced 1 KiB row read shared by the whole block through L2), reduces (distance, index) to the
+// minimum with the lowest index on ties (torch.argmin), then subtracts the chosen codeword.  Squared distances
+// are summed directly as (res - e)^2 in fp32 (no |x|^2 + |e|^2 - 2 x.e cancellation).
+constexpr int RVQ_T = 256, RVQ_MAXPER = 16, RVQ_MAXD = 1024;
+
+__global__ __launch_bounds__(RVQ_T) void rvq_encode_k(const float* __restrict__ x, long long ldx,
+                                                      const float* __restrict__ tab, const float* __restrict__ tabT,
+                                                      int Q, int cb, int D, int* __restrict__ codes, long long codes_ld) {
+  __shared__ float res[RVQ_MAXD];
+  __shared__ float bd[RVQ_T / 64];
+  __shared__ int bi[RVQ_T / 64];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int d = tid; d < D; d += RVQ_T) res[d] = x[(long long)row * ldx + d];
+  __syncthreads();
+  const int per = cb / RVQ_T;  // host guarantees cb % 256 == 0 and per <= RVQ_MAXPER, or handles the tail below
+  const int npc = (cb + RVQ_T - 1) / RVQ_T;
+  for (int q = 0; q < Q; ++q) {
+    const float* tq = tabT + (size_t)q * D * cb;
+    float acc[RVQ_MAXPER];
+#pragma unroll
+    for (int j = 0; j < RVQ_MAXPER; ++j) acc[j] = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float r = res[d];
+      const float* tr = tq + (size_t)d * cb + tid;
+#pragma unroll
+      for (int j = 0; j < RVQ_MAXPER; ++j) {
+        if (j < npc && tid + j * RVQ_T < cb) {
+          const float e = r - tr[j * RVQ_T];
+          acc[j] = fmaf(e, e, acc[j]);
+        }
+      }
+    }
+    (void)per;
+    float best = INFINITY;
+    int bidx = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < RVQ_MAXPER; ++j) {
+      const int c = tid + j * RVQ_T;
+      if (j < npc && c < cb && acc[j] < best) { best = acc[j]; bidx = c; }  // increasing c: strict < keeps lowest
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bidx, o, 64);
+      if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+    }
+    if (lane == 0) { bd[wv] = best; bi[wv] = bidx; }
+    __syncthreads();
+    float fb = bd[0];
+    int fi = bi[0];
+#pragma unroll
+    for (int w = 1; w < RVQ_T / 64; ++w)
+      if (bd[w] < fb || (bd[w] == fb && bi[w] < fi)) { fb = bd[w]; fi = bi[w]; }
+    if (tid == 0) codes[(long long)row * codes_ld + q] = fi;
+    const float* e = tab + ((size_t)q * cb + fi) * D;
+    for (int d = tid; d < D; d += RVQ_T) res[d] -= e[d];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// log-mel: one block per frame; magnitudes of the nbin DFT bins into LDS, then each thread one mel band
+constexpr int MEL_MAXBIN = 1040;
+
+__global__ __launch_bounds__(256) void mel_logmag_k(const float* __restrict__ spec, long long ld_spec, int nbin,
+                                                    const float* __restrict__ basis, int nmel, float* __restrict__ out,
+                                                    long long ldo) {
+  __shared__ float mag[MEL_MAXBIN];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const float* s = spec + (long long)f * ld_spec;
+  for (int k = tid; k < nbin; k += 256) {
+    const float re = s[2 * k], im = s[2 * k + 1];
+    mag[k] = sqrtf(re * re + im * im + 1e-9f);
+  }
+  __syncthreads();
+  for (int m = tid; m < nmel; m += 256) {
+    const float* br = basis + (long long)m * nbin;
+    float acc = 0.f;
+    for (int k = 0; k < nbin; ++k) acc = fmaf(br[k], mag[k], acc);
+    out[(long long)f * ldo + m] = logf(fmaxf(acc, 1e-5f));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// time statistics: one thread per (item, channel), loops over time (channel-contiguous => coalesced rows)
+template <typename T>
+__global__ void time_stats_k(const T* __restrict__ x, long long ldx, const float* __restrict__ lg, long long ldl, int B,
+                             int Tn, int C, float eps, float* __restrict__ mean_out, float* __restrict__ std_out,
+                             long long ld_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+  if (c >= C) return;
+  const T* xc = x + (long long)b * Tn * ldx + c;
+  float mx = 0.f, inv = 1.0f / (float)Tn;
+  const float* lc = lg ? lg + (long long)b * Tn * ldl + c : nullptr;
+  if (lc) {
+    mx = -INFINITY;
+    for (int t = 0; t < Tn; ++t) mx = fmaxf(mx, lc[(long long)t * ldl]);
+    float se = 0.f;
+    for (int t = 0; t < Tn; ++t) se += expf(lc[(long long)t * ldl] - mx);
+    inv = 1.0f / se;
+  }
+  float mean = 0.f;
+  for (int t = 0; t < Tn; ++t) {
+    const float wt = lc ? expf(lc[(long long)t * ldl] - mx) * inv : inv;
+    mean = fmaf(wt, to_f(xc[(long long)t * ldx]), mean);
+  }
+  mean_out[(long long)b * ld_out + c] = mean;
+  if (!std_out) return;
+  float var = 0.f;
+  for (int t = 0; t < Tn; ++t) {
+    const float wt = lc ? expf(lc[(long long)t * ldl] - mx) * inv : inv;
+    const float d = to_f(xc[(long long)t * ldx]) - mean;
+    var = fmaf(wt, d * d, var);
+  }
+  std_out[(long long)b * ld_out + c] = sqrtf(fmaxf(var, eps));
+}
+
+template <typename T>
+__global__ void scale_add_k(const T* __restrict__ x, long long ldx, const float* __restrict__ s, long long lds,
+                            const T* __restrict__ res, long long ldr, int Tn, int C, long long total,
+                            T* __restrict__ out, long long ldo) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int c = (int)(idx % C);
+  const long long bt = idx / C;
+  const int b = (int)(bt / Tn);
+  const float v = to_f(x[bt * ldx + c]) * s[(long long)b * lds + c] + to_f(res[bt * ldr + c]);
+  out[bt * ldo + c] = from_f<T>(v);
+}
+
+template <typename T>
+__global__ void bcast_rows_k(const float* __restrict__ v, long long ldv, int Tn, int W, long long total,
+                             T* __restrict__ out, long long ldo) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int w = (int)(idx % W);
+  const long long bt = idx / W;
+  const int b = (int)(bt / Tn);
+  out[bt * ldo + w] = from_f<T>(v[(long long)b * ldv + w]);
+}
+
+inline unsigned nblk(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" int qt_pad_time(const void* x, long long ldx, const void* x2, long long ldx2, int dtype, int B, int T, int C,
+                           int left, int right, int mode, int t_total, void* out, long long ldo, void* stream) {
+  if (!x || !out || B <= 0 || T <= 0 || C <= 0 || left < 0 || right < 0) return QT_ERR_ARG;
+  if (t_total < T + left + right || mode < QT_PAD_ZERO || mode > QT_PAD_REPLICATE) return QT_ERR_SHAPE;
+  if (mode == QT_PAD_REFLECT && (left >= T || right >= T)) return QT_ERR_SHAPE;  // torch reflect pad limit
+  const long long tot = (long long)B * t_total * C;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QT_F32)
+    hipLaunchKernelGGL(pad_time_k<float>, dim3(nblk(tot)), dim3(256), 0, s, (const float*)x, ldx, (const float*)x2, ldx2,
+                       B, T, C, left, right, mode, t_total, (float*)out, ldo);
+  else if (dtype == QT_BF16)
+    hipLaunchKernelGGL(pad_time_k<bf16_t>, dim3(nblk(tot)), dim3(256), 0, s, (const bf16_t*)x, ldx, (const bf16_t*)x2,
+                       ldx2, B, T, C, left, right, mode, t_total, (bf16_t*)out, ldo);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_zero_tail(void* x, int dtype, int B, int Tp, int v, int C, long long ldx, void* stream) {
+  if (!x || B <= 0 || C <= 0 || v < 0 || v > Tp) return QT_ERR_ARG;
+  if (v == Tp) return QT_OK;
+  const long long tot = (long long)B * (Tp - v) * C;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QT_F32) hipLaunchKernelGGL(zero_tail_k<float>, dim3(nblk(tot)), dim3(256), 0, s, (float*)x, B, Tp, v, C, ldx);
+  else if (dtype == QT_BF16)
+    hipLaunchKernelGGL(zero_tail_k<bf16_t>, dim3(nblk(tot)), dim3(256), 0, s, (bf16_t*)x, B, Tp, v, C, ldx);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_layernorm(const float* x, long long ldx, const float* w, const float* b, float eps, void* out,
+                            int o_dtype, long long ldo, int M, int N, void* stream) {
+  if (!x || !w || !b || !out || M <= 0 || N <= 0) return QT_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (o_dtype == QT_F32) hipLaunchKernelGGL(layernorm_k<float>, dim3(M), dim3(256), 0, s, x, ldx, w, b, eps, (float*)out, ldo, N);
+  else if (o_dtype == QT_BF16)
+    hipLaunchKernelGGL(layernorm_k<bf16_t>, dim3(M), dim3(256), 0, s, x, ldx, w, b, eps, (bf16_t*)out, ldo, N);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_rvq_encode(const float* x, long long ldx, const float* tab, const float* tabT, int Q, int cb, int D,
+                             int R, int* codes, long long codes_ld, void* stream) {
+  if (!x || !tab || !tabT || !codes || Q < 0 || R < 0) return QT_ERR_ARG;
+  if (cb <= 0 || cb > RVQ_T * RVQ_MAXPER || D <= 0 || D > RVQ_MAXD) return QT_ERR_SHAPE;
+  if (Q == 0 || R == 0) return QT_OK;
+  hipLaunchKernelGGL(rvq_encode_k, dim3(R), dim3(RVQ_T), 0, (hipStream_t)stream, x, ldx, tab, tabT, Q, cb, D, codes,
+                     codes_ld);
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_mel_logmag(const float* spec, long long ld_spec, int F, int nbin, const float* basis, int nmel,
+                             float* out, long long ldo, void* stream) {
+  if (!spec || !basis || !out || F < 0 || nmel <= 0) return QT_ERR_ARG;
+  if (nbin <= 0 || nbin > MEL_MAXBIN || ld_spec < 2LL * nbin) return QT_ERR_SHAPE;
+  if (F == 0) return QT_OK;
+  hipLaunchKernelGGL(mel_logmag_k, dim3(F), dim3(256), 0, (hipStream_t)stream, spec, ld_spec, nbin, basis, nmel, out, ldo);
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_time_stats(const void* x, int dtype, long long ldx, const float* logits, long long ldl, int B, int T,
+                             int C, float eps, float* mean_out, float* std_out, long long ld_out, void* stream) {
+  if (!x || !mean_out || B <= 0 || T <= 0 || C <= 0) return QT_ERR_ARG;
+  const dim3 grid(nblk(C, 64), B);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QT_F32)
+    hipLaunchKernelGGL(time_stats_k<float>, grid, dim3(64), 0, s, (const float*)x, ldx, logits, ldl, B, T, C, eps,
+                       mean_out, std_out, ld_out);
+  else if (dtype == QT_BF16)
+    hipLaunchKernelGGL(time_stats_k<bf16_t>, grid, dim3(64), 0, s, (const bf16_t*)x, ldx, logits, ldl, B, T, C, eps,
+                       mean_out, std_out, ld_out);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_scale_add(const void* x, long long ldx, const float* sc, long long lds, const void* res, long long ldr,
+                            int dtype, int B, int T, int C, void* out, long long ldo, void* stream) {
+  if (!x || !sc || !res || !out || B <= 0 || T <= 0 || C <= 0) return QT_ERR_ARG;
+  const long long tot = (long long)B * T * C;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QT_F32)
+    hipLaunchKernelGGL(scale_add_k<float>, dim3(nblk(tot)), dim3(256), 0, s, (const float*)x, ldx, sc, lds,
+                       (const float*)res, ldr, T, C, tot, (float*)out, ldo);
+  else if (dtype == QT_BF16)
+    hipLaunchKernelGGL(scale_add_k<bf16_t>, dim3(nblk(tot)), dim3(256), 0, s, (const bf16_t*)x, ldx, sc, lds,
+                       (const bf16_t*)res, ldr, T, C, tot, (bf16_t*)out, ldo);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}
+
+extern "C" int qt_bcast_rows(const float* v, long long ldv, int B, int T, int W, void* out, int o_dtype, long long ldo,
+                             void* stream) {
+  if (!v || !out || B <= 0 || T <= 0 || W <= 0) return QT_ERR_ARG;
+  const long long tot = (long long)B * T * W;
+  hipStream_t s = (hipStream_t)stream;
+  if (o_dtype == QT_F32)
+    hipLaunchKernelGGL(bcast_rows_k<float>, dim3(nblk(tot)), dim3(256), 0, s, v, ldv, T, W, tot, (float*)out, ldo);
+  else if (o_dtype == QT_BF16)
+    hipLaunchKernelGGL(bcast_rows_k<bf16_t>, dim3(nblk(tot)), dim3(256), 0, s, v, ldv, T, W, tot, (bf16_t*)out, ldo);
+  else return QT_ERR_DTYPE;
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}

@@ -34,6 +34,7 @@ struct GemmP {
   int ntl;                      // 1: non-temporal weight loads (decode GEMV over >= 16 MiB of weights)
   unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
   const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
+  int a_elu;                    // ELU on A (tokenizer encoder convs)
 };
 
 // SnakeBeta exactly as qt_snake computes it (fp32 math on the stored activation)
@@ -65,6 +66,10 @@ QT_DEV void load_a(const GemmP& p, int m, int kk, float* v) {
     src = A + row * p.lda + kk;
   }
   if constexpr (E == 8) load8f(src, v); else load4f(src, v);
+  if (p.a_elu) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = elu_f(v[i]);
+  }
   if (p.sn_a) {
     const int c0 = p.taps > 0 ? (kk % p.cin_pad) : kk;
 #pragma unroll
@@ -162,8 +167,7 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
       x *= rsqrtf(s / (float)p.Klog + p.eps);
     }
     x += bias;
-    if (p.act == QT_ACT_SILU) x = silu_f(x);
-    else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+    x = act_f(x, p.act);
     x *= cs;
     v[i] = x;
   }
@@ -320,8 +324,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     float x = v[i];
     if (NORM) x *= rsqrtf(ssr[i] / (float)p.Klog + p.eps);
     x += bias;
-    if (p.act == QT_ACT_SILU) x = silu_f(x);
-    else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+    x = act_f(x, p.act);
     v[i] = x * cs;
   }
   OT* out = (OT*)p.out;
@@ -399,6 +402,10 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       const int q = tid + i * 256, r = q >> 2, ch = c * IG_KC + (q & 3) * 8;
       if (r >= WR) continue;
       float* v = stg[i];
+      if (p.a_elu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = elu_f(v[e]);
+      }
       if (p.sn_a && ch < cin) {  // bf16 operand: the hardware sine's error is far below the bf16 rounding
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -486,8 +493,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
         float x = acc[i][q][e];
         if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
         x += bias;
-        if (p.act == QT_ACT_SILU) x = silu_f(x);
-        else if (p.act == QT_ACT_GELU) x = gelu_f(x);
+        x = act_f(x, p.act);
         v[e] = x * cs;
       }
       if (p.epi == QT_EPI_SWIGLU) {
@@ -543,6 +549,7 @@ __global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
       float v = 0.f;
       if (ti >= 0 && ti < p.t_in && c < p.cin) {
         v = to_f(A[(long long)ti * p.lda + c]);
+        if (p.a_elu) v = elu_f(v);
         if (p.sn_a) v = snake1(v, p.sn_a[c], p.sn_ib[c]);
         if (sizeof(WT) == 2) v = __uint_as_float((unsigned)f2bf(v) << 16);  // bf16 operand, as the MFMA paths
       }
@@ -588,7 +595,7 @@ template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
-  if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr) {
+  if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr && !p.a_elu) {
     const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
     if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
     else if (kts >= 16 && p.wpb_max >= 8) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
@@ -670,6 +677,9 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
   p.sn_a = a->snake_alpha; p.sn_ib = a->snake_inv_beta;
   if ((p.sn_a == nullptr) != (p.sn_ib == nullptr)) return QT_ERR_ARG;
+  if (a->a_act != QT_AACT_NONE && a->a_act != QT_AACT_ELU) return QT_ERR_ARG;
+  if (a->act < QT_ACT_NONE || a->act > QT_ACT_RELU_TANH) return QT_ERR_ARG;
+  p.a_elu = a->a_act == QT_AACT_ELU;
   static const int no_ig = [] { const char* e = getenv("QT_NO_IGEMM"); return e ? atoi(e) : 0; }();
   p.no_igemm = no_ig;
   // weights streamed once per frame (talker-size matrices) bypass cache retention so the re-read code-predictor

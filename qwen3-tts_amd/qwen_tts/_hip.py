@@ -16,7 +16,9 @@ LIB_PATH = os.environ.get("QWEN3TTS_AMD_LIB",
                           os.path.join(os.path.dirname(HERE), "lib", "libqwen3tts_amd.so"))
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_SILU, ACT_GELU = 0, 1, 2
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_RELU, ACT_SIGMOID, ACT_RELU_TANH = 0, 1, 2, 3, 4, 5
+AACT_NONE, AACT_ELU = 0, 1
+PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
 EPI_STORE, EPI_ADD, EPI_SWIGLU = 0, 1, 2
 ERRORS = {-1: "bad argument", -2: "bad shape", -3: "unsupported dtype", -4: "launch failed"}
 
@@ -30,7 +32,7 @@ class GemmArgs(ctypes.Structure):
                 ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
                 ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int),
                 ("ws", c_void_p), ("ws_bytes", c_ll), ("splitk", c_int),
-                ("snake_alpha", c_void_p), ("snake_inv_beta", c_void_p)]
+                ("snake_alpha", c_void_p), ("snake_inv_beta", c_void_p), ("a_act", c_int)]
 
 GEMM_WS_MIN = 4 << 20  # QT_GEMM_WS_MIN
 
@@ -77,7 +79,9 @@ class MlpArgs(ctypes.Structure):
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
-           "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm"]
+           "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
+           "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_mel_logmag", "qt_time_stats",
+           "qt_scale_add", "qt_bcast_rows"]
 
 _LIB = None
 
@@ -103,6 +107,14 @@ def load_library(path: str = LIB_PATH):
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
         "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
+        "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
+        "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
+        "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],
+        "qt_rvq_encode": [P, c_ll, P, P, c_int, c_int, c_int, c_int, P, c_ll, P],
+        "qt_mel_logmag": [P, c_ll, c_int, c_int, P, c_int, P, c_ll, P],
+        "qt_time_stats": [P, c_int, c_ll, P, c_ll, c_int, c_int, c_int, c_float, P, P, c_ll, P],
+        "qt_scale_add": [P, c_ll, P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, P, c_ll, P],
+        "qt_bcast_rows": [P, c_ll, c_int, c_int, c_int, P, c_int, c_ll, P],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -1,7 +1,8 @@
 """Drop-in `Qwen3TTSModel` (reference: qwen_tts/inference/qwen3_tts_model.py, `W` below).
 
 Same public surface and semantics: from_pretrained, generate_custom_voice / generate_voice_design /
-generate_voice_clone (with a prepared voice_clone_prompt), get_supported_speakers / languages, kwargs
+generate_voice_clone (from reference audio or a prepared voice_clone_prompt), create_voice_clone_prompt,
+get_supported_speakers / languages, kwargs
 precedence of `_merge_generate_kwargs` (W:287-352), validation errors (W:141-186), wrapper defaults
 (max_new_tokens 2048, non_streaming_mode True/True/False) and the 0.6B instruct drop (W:799).
 New: `stream()` yields (pcm chunk, sr) per utterance as soon as its codes are decoded.
@@ -16,8 +17,10 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 import numpy as np
 import torch
 
+from .. import audio as _audio
 from ..model import TTSModel
 from ..text import load_processor
+from ..speaker import speaker_specs
 from ..weights import is_preset_dir, load_safetensors, read_json, resolve_path, synthetic, talker_specs
 from .qwen3_tts_tokenizer import Qwen3TTSTokenizer, _dtype_name
 
@@ -60,7 +63,10 @@ class Qwen3TTSModel:
         if not W:
             if not is_preset_dir(d):
                 raise FileNotFoundError(f"no model*.safetensors in checkpoint directory {d!r}")
-            W = synthetic(talker_specs(cfg), dev, seed)
+            specs = talker_specs(cfg)
+            if cfg.get("tts_model_type") == "base":
+                specs = specs + speaker_specs(cfg)
+            W = synthetic(specs, dev, seed)
         with torch.cuda.device(dev):
             m = TTSModel(cfg, W, dtype=_dtype_name(dtype), device=dev, generate_config=gen)
         del W
@@ -142,12 +148,38 @@ class Qwen3TTSModel:
         return self.model.speech_tokenizer.decode([{"audio_codes": c} for c in codes_list])
 
     # ---------------------------------------------------------------- voice clone (W:356-633)
-    def create_voice_clone_prompt(self, ref_audio, ref_text=None, x_vector_only_mode=False):
+    def create_voice_clone_prompt(self, ref_audio, ref_text=None, x_vector_only_mode=False) -> List[VoiceClonePromptItem]:
+        """W:356-458: reference audio -> ref_code (12 Hz tokenizer encode, HIP) + x-vector (mel + ECAPA, HIP)."""
         if self.model.tts_model_type != "base":
-            raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
-                             "create_voice_clone_prompt, Please check Model Card or Readme for more details.")
-        raise NotImplementedError("reference-audio encode (Mimi) + ECAPA speaker encoder are the next tier of this "
-                                  "build (SURVEY.md §8f-2); pass a prepared voice_clone_prompt instead")
+            raise ValueError(f"model with \ntokenizer_type: {self.model.tokenizer_type}\n"
+                             f"tts_model_size: {self.model.tts_model_size}\n"
+                             f"tts_model_type: {self.model.tts_model_type}\n"
+                             "does not support create_voice_clone_prompt, Please check Model Card or Readme for more details.")
+        ref_audio_list = self._ensure_list(ref_audio)
+        ref_text_list = self._ensure_list(ref_text) if isinstance(ref_text, list) else [ref_text] * len(ref_audio_list)
+        xvec_list = self._ensure_list(x_vector_only_mode) if isinstance(x_vector_only_mode, list) else \
+            [x_vector_only_mode] * len(ref_audio_list)
+        if len(ref_text_list) != len(ref_audio_list) or len(xvec_list) != len(ref_audio_list):
+            raise ValueError(f"Batch size mismatch: ref_audio={len(ref_audio_list)}, ref_text={len(ref_text_list)}, "
+                             f"x_vector_only_mode={len(xvec_list)}")
+        normalized = _audio.normalize_pairs(ref_audio_list)
+        srs = [sr for _, sr in normalized]
+        tok = self.model.speech_tokenizer
+        if len(set(srs)) == 1:
+            ref_codes = tok.encode([w for w, _ in normalized], sr=srs[0]).audio_codes
+        else:
+            ref_codes = [tok.encode(w, sr=sr).audio_codes[0] for w, sr in normalized]
+        items = []
+        spk_sr = self.model.speaker_encoder_sample_rate
+        for i, ((wav, sr), code, rtext, xvec_only) in enumerate(zip(normalized, ref_codes, ref_text_list, xvec_list)):
+            if not xvec_only and (rtext is None or rtext == ""):
+                raise ValueError(f"ref_text is required when x_vector_only_mode=False (ICL mode). Bad index={i}")
+            wav_rs = _audio.resample(wav, sr, spk_sr) if sr != spk_sr else wav
+            spk = self.model.extract_speaker_embedding(audio=wav_rs, sr=spk_sr)
+            items.append(VoiceClonePromptItem(ref_code=None if xvec_only else code, ref_spk_embedding=spk,
+                                              x_vector_only_mode=bool(xvec_only), icl_mode=bool(not xvec_only),
+                                              ref_text=rtext))
+        return items
 
     def _prompt_items_to_voice_clone_prompt(self, items: List[VoiceClonePromptItem]) -> Dict[str, Any]:
         return dict(ref_code=[it.ref_code for it in items], ref_spk_embedding=[it.ref_spk_embedding for it in items],

@@ -3,7 +3,9 @@
 decode() accepts exactly the reference's input forms (Z:286-329: encode output / dict / list of dicts,
 torch or numpy codes, [T,16] or [B,T,16]), right-pads a batch with code 0 (Z:329) and returns
 (list of 1-D float32 numpy wavs, 24000).  The decoder runs on the MI355X HIP kernels (qwen_tts/codec.py).
-encode() (Mimi encoder, 12 Hz) is the next tier and raises NotImplementedError.
+encode() (Z:208-257) takes the reference's audio forms, right-pads the batch like its
+EncodecFeatureExtractor and runs the 12 Hz encoder on the HIP kernels (qwen_tts/encoder.py), returning an
+object with `.audio_codes` = list of int64 [T_i, 16] device tensors (Qwen3TTSTokenizerV2EncoderOutput).
 """
 from __future__ import annotations
 
@@ -14,8 +16,23 @@ import numpy as np
 import torch
 from torch.nn.utils.rnn import pad_sequence
 
+from .. import audio as _audio
 from ..codec import CodecDecoder
+from ..encoder import TokenizerEncoder, encoder_specs
 from ..weights import codec_specs, is_preset_dir, load_safetensors, read_json, resolve_path, synthetic
+
+
+class EncoderOutput(dict):
+    """Qwen3TTSTokenizerV2EncoderOutput (K:54-60): attribute and key access to `audio_codes`."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def to_tuple(self):
+        return (self["audio_codes"],)
 
 
 def _dtype_name(dtype) -> str:
@@ -32,6 +49,7 @@ class Qwen3TTSTokenizer:
         self.feature_extractor = None
         self.config = None
         self.device = None
+        self.encoder = None
 
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path: str, device_map="cuda:0", dtype=None, weights=None,
@@ -49,15 +67,29 @@ class Qwen3TTSTokenizer:
         if not W:
             if not is_preset_dir(d):
                 raise FileNotFoundError(f"no model*.safetensors in tokenizer directory {d!r}")
-            W = synthetic(codec_specs(ccfg), dev, seed)
+            W = synthetic(codec_specs(ccfg) + encoder_specs(ccfg), dev, seed)
         inst.config = ccfg
         inst.device = dev
+        pre = os.path.join(d, "preprocessor_config.json")
+        inst.feature_extractor = read_json(pre) if os.path.exists(pre) else {"sampling_rate": 24000}
         with torch.cuda.device(dev):
             inst.model = CodecDecoder(ccfg, W, dtype=_dtype_name(dtype), device=dev)
+            if "encoder.encoder.layers.0.conv.weight" in W:
+                inst.encoder = TokenizerEncoder(ccfg, W, dtype=_dtype_name(dtype), device=dev)
         return inst
 
     def encode(self, audios, sr: Optional[int] = None, return_dict: bool = True):
-        raise NotImplementedError("12 Hz encoder (Mimi) is the next tier of this build (SURVEY.md §8f-2)")
+        """Z:208-257: wav path / base64 / np.ndarray (with sr) or lists of them -> EncoderOutput(audio_codes=[...])
+        with int64 [T_i, 16] codes on the device (T_i = ceil(len_i / 1920) at 24 kHz)."""
+        if self.encoder is None:
+            raise ValueError("this tokenizer checkpoint has no encoder weights (encoder.* in model.safetensors)")
+        target = int(self.feature_extractor.get("sampling_rate", 24000))
+        wavs = _audio.normalize_at(audios, sr, target)
+        with torch.inference_mode(), torch.cuda.device(self.device):
+            codes = self.encoder.encode([torch.from_numpy(np.ascontiguousarray(w)) for w in wavs])
+        if not return_dict:
+            return (codes,)
+        return EncoderOutput(audio_codes=codes)
 
     def decode(self, encoded) -> Tuple[List[np.ndarray], int]:
         """Z:259-365."""

@@ -139,7 +139,8 @@ class use_workspace:
 
 
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
-         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0, snake=None):
+         act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0, snake=None,
+         a_act=_hip.AACT_NONE):
     """conv = (t_in, t_out, t_off, dil) for implicit-conv weights.  splitk: 0 auto, 1 off, n forced
     (decode GEMV only, needs gemm_workspace(device) allocated).  snake = (alpha, inv_beta): SnakeBeta applied
     to A per input channel inside the GEMM (fused codec activation)."""
@@ -155,6 +156,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.out, a.ldo = ptr(out), ldo
     if snake is not None:
         a.snake_alpha, a.snake_inv_beta = ptr(snake[0]), ptr(snake[1])
+    a.a_act = a_act
     ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
     if ws is not None and M <= 16 and not W.taps:
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
@@ -301,3 +303,44 @@ def rope_tables(head_dim: int, theta: float, npos: int, device):
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).to(dtype=torch.float) / head_dim))
     f = torch.arange(npos, dtype=torch.float32)[:, None] * inv[None, :]
     return f.cos().contiguous().to(device), f.sin().contiguous().to(device)
+
+
+# ---- voice-clone front end (csrc/frontend.hip) ----
+def pad_time(x, B, T, C, left, right, mode, out, t_total=None, x2=None, ldx=None, ldx2=None, ldo=None):
+    t_total = T + left + right if t_total is None else t_total
+    check(_hip.lib().qt_pad_time(ptr(x), ldx or C, ptr(x2), ldx2 or C, _hip.dtype_code(x.dtype), B, T, C, left, right,
+                                 mode, t_total, ptr(out), ldo or C, stream()), "qt_pad_time")
+
+
+def zero_tail(x, B, Tp, v, C, ldx=None):
+    check(_hip.lib().qt_zero_tail(ptr(x), _hip.dtype_code(x.dtype), B, Tp, v, C, ldx or C, stream()), "qt_zero_tail")
+
+
+def layernorm(x, w, b, eps, out, M, N, ldx=None, ldo=None):
+    check(_hip.lib().qt_layernorm(ptr(x), ldx or N, ptr(w), ptr(b), eps, ptr(out), _hip.dtype_code(out.dtype),
+                                  ldo or N, M, N, stream()), "qt_layernorm")
+
+
+def rvq_encode(x, ldx, tab, tabT, Q, cb, D, R, codes, codes_ld):
+    check(_hip.lib().qt_rvq_encode(ptr(x), ldx, ptr(tab), ptr(tabT), Q, cb, D, R, ptr(codes), codes_ld, stream()),
+          "qt_rvq_encode")
+
+
+def mel_logmag(spec, ld_spec, F_, nbin, basis, nmel, out, ldo=None):
+    check(_hip.lib().qt_mel_logmag(ptr(spec), ld_spec, F_, nbin, ptr(basis), nmel, ptr(out), ldo or nmel, stream()),
+          "qt_mel_logmag")
+
+
+def time_stats(x, B, T, C, mean_out, std_out=None, logits=None, eps=1e-12, ldx=None, ldl=None, ld_out=None):
+    check(_hip.lib().qt_time_stats(ptr(x), _hip.dtype_code(x.dtype), ldx or C, ptr(logits), ldl or C, B, T, C, eps,
+                                   ptr(mean_out), ptr(std_out), ld_out or C, stream()), "qt_time_stats")
+
+
+def scale_add(x, s, res, B, T, C, out, ldx=None, lds=None, ldr=None, ldo=None):
+    check(_hip.lib().qt_scale_add(ptr(x), ldx or C, ptr(s), lds or C, ptr(res), ldr or C, _hip.dtype_code(x.dtype),
+                                  B, T, C, ptr(out), ldo or C, stream()), "qt_scale_add")
+
+
+def bcast_rows(v, B, T, W, out, ldv=None, ldo=None):
+    check(_hip.lib().qt_bcast_rows(ptr(v), ldv or W, B, T, W, ptr(out), _hip.dtype_code(out.dtype), ldo or W, stream()),
+          "qt_bcast_rows")

@@ -28,6 +28,19 @@ class TTSModel:
         self.supported_speakers = list((self.tc.get("spk_id") or {}).keys())
         self.supported_languages = ["auto"] + [k for k in (self.tc.get("codec_language_id") or {}) if "dialect" not in k]
         self.speaker_encoder_sample_rate = config.get("speaker_encoder_config", {}).get("sample_rate", 24000)
+        self.speaker_encoder = None
+        if self.tts_model_type == "base" and "speaker_encoder.fc.weight" in weights:  # M:1821-1824
+            from .speaker import SpeakerEncoder
+            self.speaker_encoder = SpeakerEncoder(config, weights, dtype=dtype, device=self.device)
+
+    @torch.inference_mode()
+    def extract_speaker_embedding(self, audio, sr):
+        """M:1940-1954: 24 kHz mono float32 waveform -> x-vector [enc_dim] (device, fp32)."""
+        assert sr == 24000, "Only support 24kHz audio"
+        if self.speaker_encoder is None:
+            raise ValueError("no speaker encoder loaded (tts_model_type != 'base', or its weights are absent)")
+        with torch.cuda.device(self.device):
+            return self.speaker_encoder.embed(audio)
 
     def get_supported_speakers(self):
         return self.supported_speakers

@@ -74,10 +74,17 @@ def synthetic(specs, device, seed=1234) -> Dict[str, torch.Tensor]:
     out = {}
     for name, shape in specs:
         n = lambda: torch.randn(shape, generator=g, device=device)  # noqa: E731
-        if name.endswith("_codebook.cluster_usage"):
+        if name.endswith("_codebook.cluster_usage") or name.endswith(".codebook.cluster_usage"):
             t = torch.rand(shape, generator=g, device=device) * 1.5 + 0.5
-        elif name.endswith("_codebook.embedding_sum"):
+        elif name.endswith("_codebook.embedding_sum") or name.endswith(".codebook.embed_sum"):
             t = n()
+        elif name.endswith(".codebook.initialized"):
+            t = torch.ones(shape, device=device)
+        elif (name.startswith("encoder.") or name.startswith("speaker_encoder.")) and name.endswith("weight") \
+                and len(shape) in (2, 3) and "norm" not in name:
+            fan = shape[1] * (shape[2] if len(shape) == 3 else 1)
+            gain = 1.4 if name.startswith("speaker_encoder.") else (0.5 if name.endswith("block.3.conv.weight") else 1.0)
+            t = gain * n() / fan ** 0.5
         elif name.endswith(".alpha") or name.endswith(".beta"):
             t = 0.1 * n()
         elif name.endswith("layer_scale.scale") or name.endswith(".gamma"):

@@ -72,3 +72,25 @@ def gen_kwargs(case):
                 subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9, repetition_penalty=1.05)
 
 
+
+
+def ref_audio(n, seed):
+    """Deterministic 24 kHz reference clip (voice-clone front end cases): two partials with a slow tremolo
+    plus seeded noise, float32 in about [-0.45, 0.45].  Pure float64 numpy arithmetic, so the GPU box
+    rebuilds bit-identical inputs."""
+    t = np.arange(n, dtype=np.float64) / 24000.0
+    g = np.random.default_rng([seed, 23])
+    f0 = 110.0 + 20.0 * (seed % 7)
+    x = 0.25 * np.sin(2 * np.pi * f0 * t) * (1.0 + 0.5 * np.sin(2 * np.pi * 3.0 * t))
+    x += 0.1 * np.sin(2 * np.pi * 7.3 * f0 * t + 0.3)
+    x += 0.05 * g.standard_normal(n)
+    return x.astype(np.float32)
+
+
+def frontend_cases():
+    """Encoder (Mimi) batches and speaker-encoder clips: lengths in samples at 24 kHz."""
+    return {
+        "tiny": dict(enc={"single": [31234], "batch": [40000, 17000], "exact": [3840], "short": [1000]},
+                     spk=[24000, 7777]),
+        "full": dict(enc={"single": [72000], "batch": [50000, 72000]}, spk=[72000]),
+    }

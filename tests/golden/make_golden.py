@@ -30,7 +30,7 @@ sys.path.insert(0, HERE)
 sys.path.insert(0, REPO)
 
 import ref_shim  # noqa: E402
-from cases import gen_kwargs, make_inputs, talker_cases  # noqa: E402,F401
+from cases import frontend_cases, gen_kwargs, make_inputs, ref_audio, talker_cases  # noqa: E402,F401
 from oracle import load_preset  # noqa: E402
 from oracle.weights import synth_param  # noqa: E402
 
@@ -169,13 +169,80 @@ def make_codec(preset, cases, fname):
     np.savez_compressed(os.path.join(HERE, fname), **out)
 
 
+class _SpeakerModelView:
+    """The attributes Qwen3TTSForConditionalGeneration.extract_speaker_embedding reads (M:1940-1954)."""
+
+    def __init__(self, enc):
+        self.speaker_encoder = enc
+        self.device = torch.device("cpu")
+        self.dtype = torch.float32
+
+
+def make_frontend(preset, kind, fname):
+    """Voice-clone front end: reference Qwen3TTSTokenizerV2Model.encode (K:960-990, Mimi from transformers) and
+    extract_speaker_embedding (M:1940-1954) on seeded synthetic weights.  librosa is absent: its slaney mel
+    filterbank is supplied by oracle.speaker.slaney_mel_filterbank (a restatement; see that module)."""
+    from oracle.speaker import slaney_mel_filterbank
+    mdl, cfgm, mtok, ctok = ref_shim.load_reference()
+    mdl.librosa_mel_fn = lambda sr, n_fft, n_mels, fmin, fmax: slaney_mel_filterbank(sr, n_fft, n_mels, fmin, fmax)
+    cfg, ccfg = load_preset(preset)
+    cases = frontend_cases()[kind]
+    out = {}
+    # tokenizer encoder
+    config = ctok.Qwen3TTSTokenizerV2Config(**json.loads(json.dumps(ccfg)))
+    _eagerize(config.decoder_config)
+    torch.manual_seed(0)
+    tok = mtok.Qwen3TTSTokenizerV2Model(config).eval()
+    sd = tok.state_dict()
+    tok.load_state_dict({k: torch.from_numpy(synth_param(k, v.shape, SEED)) for k, v in sd.items()})
+    for key, lens in cases["enc"].items():
+        wavs = [ref_audio(n, 1000 + 10 * i + n % 97) for i, n in enumerate(lens)]
+        L = max(lens)
+        x = torch.zeros(len(wavs), L)
+        mask = torch.zeros(len(wavs), L, dtype=torch.long)
+        for i, w in enumerate(wavs):
+            x[i, :len(w)] = torch.from_numpy(w)
+            mask[i, :len(w)] = 1
+        t0 = time.time()
+        with torch.inference_mode():
+            enc = tok.encode(x, mask, return_dict=True)
+        for j, c in enumerate(enc.audio_codes):
+            out[f"enc/{key}/codes{j}"] = c.numpy().astype(np.int32)
+            out[f"enc/{key}/sum{j}"] = np.array(float(wavs[j].astype(np.float64).sum()))
+        print(f"  {fname}:enc/{key} frames {[c.shape[0] for c in enc.audio_codes]} ({time.time() - t0:.1f}s)")
+    # speaker encoder
+    sc = cfgm.Qwen3TTSSpeakerEncoderConfig(**cfg["speaker_encoder_config"])
+    spk = mdl.Qwen3TTSSpeakerEncoder(sc).eval()
+    sd = spk.state_dict()
+    spk.load_state_dict({k: torch.from_numpy(synth_param("speaker_encoder." + k, v.shape, SEED)) for k, v in sd.items()})
+    view = _SpeakerModelView(spk)
+    for j, n in enumerate(cases["spk"]):
+        w = ref_audio(n, 2000 + j)
+        with torch.inference_mode():
+            mel = mdl.mel_spectrogram(torch.from_numpy(w).unsqueeze(0), n_fft=1024, num_mels=128, sampling_rate=24000,
+                                      hop_size=256, win_size=1024, fmin=0, fmax=12000).transpose(1, 2)
+            emb = mdl.Qwen3TTSForConditionalGeneration.extract_speaker_embedding.__wrapped__(view, w, 24000) \
+                if hasattr(mdl.Qwen3TTSForConditionalGeneration.extract_speaker_embedding, "__wrapped__") else \
+                mdl.Qwen3TTSForConditionalGeneration.extract_speaker_embedding(view, w, 24000)
+        out[f"spk/{j}/mel"] = mel[0].numpy().astype(np.float32)
+        out[f"spk/{j}/emb"] = emb.numpy().astype(np.float32)
+        out[f"spk/{j}/sum"] = np.array(float(w.astype(np.float64).sum()))
+        print(f"  {fname}:spk/{j} mel {tuple(mel.shape)} emb {tuple(emb.shape)} |emb| {float(emb.norm()):.3f}")
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+
+
 def make_specs():
     specs = {}
-    for p in ("tiny-customvoice", "tiny-base", "1.7b-customvoice", "0.6b-customvoice"):
+    for p in ("tiny-customvoice", "tiny-base", "1.7b-customvoice", "0.6b-customvoice", "1.7b-base"):
         m, _ = build_ref_model(p, meta=True)
         specs[p] = {k: list(v.shape) for k, v in m.state_dict().items()}
         d, _ = build_ref_codec(p, meta=True)
         specs[p + "/codec"] = {"decoder." + k: list(v.shape) for k, v in d.state_dict().items()}
+        _, _, mtok, ctok = ref_shim.load_reference()
+        _, ccfg = load_preset(p)
+        with torch.device("meta"):
+            tok = mtok.Qwen3TTSTokenizerV2Model(ctok.Qwen3TTSTokenizerV2Config(**json.loads(json.dumps(ccfg))))
+        specs[p + "/encoder"] = {k: list(v.shape) for k, v in tok.state_dict().items() if k.startswith("encoder.")}
     with open(os.path.join(HERE, "param_specs.json"), "w") as f:
         json.dump(specs, f)
 
@@ -215,6 +282,9 @@ def main():
         make_codec("tiny-customvoice", {"single": [40], "batch_ragged": [23, 9], "chunked": [330]},
                    "codec_tiny.npz")
         make_codec("1.7b-customvoice", {"single": [38], "batch_ragged": [12, 5]}, "codec_full.npz")
+    if a.only in (None, "frontend"):
+        make_frontend("tiny-base", "tiny", "frontend_tiny.npz")
+        make_frontend("1.7b-base", "full", "frontend_full.npz")
     if a.full or a.only == "full":
         make_full()
 
