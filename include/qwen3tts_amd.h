@@ -240,9 +240,12 @@ int qt_layernorm(const float* x, long long ldx, const float* w, const float* b, 
 /* Residual VQ encode (MimiResidualVectorQuantizer.encode T:1050-1068 / MimiEuclideanCodebook.quantize T:985-991):
  * per row r: res = x[r]; for q < Q: code = argmin_c |res - E_q[c]|^2 (lowest index on ties), res -= E_q[code];
  * codes[r*codes_ld + q] = code.  tab [Q][cb][D] (embed_sum / clamp(cluster_usage, 1e-5)), tabT = the same
- * transposed [Q][D][cb].  D <= 1024, cb % 64 == 0. */
+ * transposed [Q][D][cb].  D <= 256, cb % 64 == 0.  ws: zero-initialised device scratch of
+ * >= qt_rvq_encode_ws_bytes(R, D, cb) bytes, one stream at a time (arrival counters re-arm themselves).
+ * Launches Q kernels (one per codebook stage); deterministic. */
+long long qt_rvq_encode_ws_bytes(int R, int D, int cb);
 int qt_rvq_encode(const float* x, long long ldx, const float* tab, const float* tabT, int Q, int cb, int D, int R,
-                  int* codes, long long codes_ld, void* stream);
+                  int* codes, long long codes_ld, void* ws, long long ws_bytes, void* stream);
 /* log-mel from a real DFT (M:451-468): spec [F][ld_spec] holds (re, im) pairs of nbin bins;
  * out[f][m] = log(max(sum_k basis[m][k] * sqrt(re^2 + im^2 + 1e-9), 1e-5)). */
 int qt_mel_logmag(const float* spec, long long ld_spec, int F, int nbin, const float* basis, int nmel, float* out,

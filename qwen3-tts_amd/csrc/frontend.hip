@@ -73,65 +73,105 @@ __global__ __launch_bounds__(256) void layernorm_k(const float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Residual VQ encode.  One 256-thread block per frame row; the residual lives in LDS.  For each codebook the
-// block scores all cb codewords (thread t owns codewords t, t+256, ...; the transposed table makes each d-step
-// one coalesced 1 KiB row read shared by the whole block through L2), reduces (distance, index) to the
-// minimum with the lowest index on ties (torch.argmin), then subtracts the chosen codeword.  Squared distances
-// are summed directly as (res - e)^2 in fp32 (no |x|^2 + |e|^2 - 2 x.e cancellation).
-constexpr int RVQ_T = 256, RVQ_MAXPER = 16, RVQ_MAXD = 1024;
+// Residual VQ encode, one launch per codebook stage q.  Grid = (cb / 64 codeword slices) x (row tiles of 32
+// frames): each block stages its slice of the transposed table [D][64] and its 32 residual rows in LDS and
+// scores all 32 x 64 (row, codeword) pairs as exact fp32 sums of (res - e)^2 (no |x|^2 + |e|^2 - 2 x.e
+// cancellation); wave w owns rows 8w..8w+7, lane j codeword j of the slice.  Per row the slice minimum
+// (lowest index on ties) goes to a partial record; the last block of the row tile to arrive (agent-scope
+// relaxed atomics + explicit vmcnt drain: coherent across the 8 XCD L2s without an L2 writeback) reduces the
+// partials in slice order, writes the code and advances the residual res = res - E_q[code] for stage q+1.
+// The stage-to-stage dependency is carried by the launch boundary.
+constexpr int RVQ_W = 64, RVQ_RB = 32, RVQ_MAXD = 256;
 
-__global__ __launch_bounds__(RVQ_T) void rvq_encode_k(const float* __restrict__ x, long long ldx,
-                                                      const float* __restrict__ tab, const float* __restrict__ tabT,
-                                                      int Q, int cb, int D, int* __restrict__ codes, long long codes_ld) {
-  __shared__ float res[RVQ_MAXD];
-  __shared__ float bd[RVQ_T / 64];
-  __shared__ int bi[RVQ_T / 64];
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int d = tid; d < D; d += RVQ_T) res[d] = x[(long long)row * ldx + d];
+struct RvqWs {
+  unsigned* cnt; float* pd; int* pi; float* res;
+};
+
+__host__ __device__ inline RvqWs rvq_ws(void* ws, int R, int D, int S) {
+  const int tiles = (R + RVQ_RB - 1) / RVQ_RB;
+  char* p = (char*)ws;
+  RvqWs w;
+  w.cnt = (unsigned*)p; p += ((size_t)tiles * sizeof(unsigned) + 255) / 256 * 256;
+  w.pd = (float*)p; p += ((size_t)R * S * sizeof(float) + 255) / 256 * 256;
+  w.pi = (int*)p; p += ((size_t)R * S * sizeof(int) + 255) / 256 * 256;
+  w.res = (float*)p;
+  return w;
+}
+
+__global__ __launch_bounds__(256) void rvq_stage_k(const float* __restrict__ x, long long ldx,
+                                                   const float* __restrict__ tab, const float* __restrict__ tabT, int q,
+                                                   int cb, int D, int R, int* __restrict__ codes, long long codes_ld,
+                                                   RvqWs ws) {
+  __shared__ float eT[RVQ_MAXD][RVQ_W + 1];
+  __shared__ float rs[RVQ_RB][RVQ_MAXD];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int s = blockIdx.x, S = gridDim.x, r0 = blockIdx.y * RVQ_RB;
+  const int nr = min(RVQ_RB, R - r0);
+  const float* tq = tabT + (size_t)q * D * cb + (size_t)s * RVQ_W;
+  for (int i = tid; i < D * RVQ_W; i += 256) eT[i / RVQ_W][i % RVQ_W] = tq[(size_t)(i / RVQ_W) * cb + (i % RVQ_W)];
+  const float* src = q == 0 ? x : ws.res;
+  const long long lds = q == 0 ? ldx : D;
+  for (int i = tid; i < RVQ_RB * D; i += 256) {
+    const int r = i / D, d = i % D;
+    rs[r][d] = r < nr ? src[(long long)(r0 + r) * lds + d] : 0.f;
+  }
   __syncthreads();
-  const int per = cb / RVQ_T;  // host guarantees cb % 256 == 0 and per <= RVQ_MAXPER, or handles the tail below
-  const int npc = (cb + RVQ_T - 1) / RVQ_T;
-  for (int q = 0; q < Q; ++q) {
-    const float* tq = tabT + (size_t)q * D * cb;
-    float acc[RVQ_MAXPER];
+  float acc[8];
 #pragma unroll
-    for (int j = 0; j < RVQ_MAXPER; ++j) acc[j] = 0.f;
-    for (int d = 0; d < D; ++d) {
-      const float r = res[d];
-      const float* tr = tq + (size_t)d * cb + tid;
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float e = eT[d][lane];
 #pragma unroll
-      for (int j = 0; j < RVQ_MAXPER; ++j) {
-        if (j < npc && tid + j * RVQ_T < cb) {
-          const float e = r - tr[j * RVQ_T];
-          acc[j] = fmaf(e, e, acc[j]);
-        }
-      }
+    for (int k = 0; k < 8; ++k) {
+      const float t = rs[wv * 8 + k][d] - e;
+      acc[k] = fmaf(t, t, acc[k]);
     }
-    (void)per;
-    float best = INFINITY;
-    int bidx = 0x7fffffff;
+  }
+  const int cidx = s * RVQ_W + lane;
 #pragma unroll
-    for (int j = 0; j < RVQ_MAXPER; ++j) {
-      const int c = tid + j * RVQ_T;
-      if (j < npc && c < cb && acc[j] < best) { best = acc[j]; bidx = c; }  // increasing c: strict < keeps lowest
+  for (int k = 0; k < 8; ++k) {
+    float bd = acc[k];
+    int bi = cidx;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float od = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    const int r = wv * 8 + k;
+    if (lane == 0 && r < nr) {
+      __hip_atomic_store(ws.pd + (size_t)(r0 + r) * S + s, bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ws.pi + (size_t)(r0 + r) * S + s, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // partials acknowledged before this block's arrival is counted
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(ws.cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (unsigned)S - 1;
+    if (last) __hip_atomic_store(ws.cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+  __syncthreads();
+  if (!last) return;
+  // last arriver: per row (one wave per row, rows strided by 4 waves) reduce the S slice minima in order
+  for (int r = wv; r < nr; r += 4) {
+    float bd = INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = lane; j < S; j += 64) {
+      const float d = __hip_atomic_load(ws.pd + (size_t)(r0 + r) * S + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int i = __hip_atomic_load(ws.pi + (size_t)(r0 + r) * S + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bidx, o, 64);
-      if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+      const float od = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
     }
-    if (lane == 0) { bd[wv] = best; bi[wv] = bidx; }
-    __syncthreads();
-    float fb = bd[0];
-    int fi = bi[0];
-#pragma unroll
-    for (int w = 1; w < RVQ_T / 64; ++w)
-      if (bd[w] < fb || (bd[w] == fb && bi[w] < fi)) { fb = bd[w]; fi = bi[w]; }
-    if (tid == 0) codes[(long long)row * codes_ld + q] = fi;
-    const float* e = tab + ((size_t)q * cb + fi) * D;
-    for (int d = tid; d < D; d += RVQ_T) res[d] -= e[d];
-    __syncthreads();
+    if (lane == 0) codes[(long long)(r0 + r) * codes_ld + q] = bi;
+    const float* e = tab + ((size_t)q * cb + bi) * D;
+    for (int d = lane; d < D; d += 64) ws.res[(long long)(r0 + r) * D + d] = rs[r][d] - e[d];
   }
 }
 
@@ -260,13 +300,26 @@ extern "C" int qt_layernorm(const float* x, long long ldx, const float* w, const
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
 }
 
+extern "C" long long qt_rvq_encode_ws_bytes(int R, int D, int cb) {
+  if (R <= 0 || D <= 0 || cb <= 0) return 0;
+  const int S = (cb + RVQ_W - 1) / RVQ_W, tiles = (R + RVQ_RB - 1) / RVQ_RB;
+  auto up = [](size_t n) { return (n + 255) / 256 * 256; };
+  return (long long)(up((size_t)tiles * 4) + up((size_t)R * S * 4) + up((size_t)R * S * 4) + (size_t)R * D * 4);
+}
+
 extern "C" int qt_rvq_encode(const float* x, long long ldx, const float* tab, const float* tabT, int Q, int cb, int D,
-                             int R, int* codes, long long codes_ld, void* stream) {
-  if (!x || !tab || !tabT || !codes || Q < 0 || R < 0) return QT_ERR_ARG;
-  if (cb <= 0 || cb > RVQ_T * RVQ_MAXPER || D <= 0 || D > RVQ_MAXD) return QT_ERR_SHAPE;
+                             int R, int* codes, long long codes_ld, void* ws, long long ws_bytes, void* stream) {
+  if (!x || !tab || !tabT || !codes || !ws || Q < 0 || R < 0) return QT_ERR_ARG;
+  if (cb <= 0 || cb % RVQ_W || D <= 0 || D > RVQ_MAXD) return QT_ERR_SHAPE;
   if (Q == 0 || R == 0) return QT_OK;
-  hipLaunchKernelGGL(rvq_encode_k, dim3(R), dim3(RVQ_T), 0, (hipStream_t)stream, x, ldx, tab, tabT, Q, cb, D, codes,
-                     codes_ld);
+  if (ws_bytes < qt_rvq_encode_ws_bytes(R, D, cb)) return QT_ERR_ARG;
+  const int S = cb / RVQ_W;
+  const RvqWs w = rvq_ws(ws, R, D, S);
+  const dim3 grid(S, (R + RVQ_RB - 1) / RVQ_RB);
+  for (int q = 0; q < Q; ++q) {
+    hipLaunchKernelGGL(rvq_stage_k, grid, dim3(256), 0, (hipStream_t)stream, x, ldx, tab, tabT, q, cb, D, R, codes,
+                       codes_ld, w);
+  }
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
 }
 

@@ -80,7 +80,7 @@ EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decod
            "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
-           "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_mel_logmag", "qt_time_stats",
+           "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
            "qt_scale_add", "qt_bcast_rows"]
 
 _LIB = None
@@ -110,7 +110,8 @@ def load_library(path: str = LIB_PATH):
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],
-        "qt_rvq_encode": [P, c_ll, P, P, c_int, c_int, c_int, c_int, P, c_ll, P],
+        "qt_rvq_encode": [P, c_ll, P, P, c_int, c_int, c_int, c_int, P, c_ll, P, c_ll, P],
+        "qt_rvq_encode_ws_bytes": [c_int, c_int, c_int],
         "qt_mel_logmag": [P, c_ll, c_int, c_int, P, c_int, P, c_ll, P],
         "qt_time_stats": [P, c_int, c_ll, P, c_ll, c_int, c_int, c_int, c_float, P, P, c_ll, P],
         "qt_scale_add": [P, c_ll, P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, P, c_ll, P],

@@ -15,7 +15,8 @@ Layout: channels-last [B][T][C] throughout, fp32 activations, weights bf16 or fp
   level's valid length right before each strided conv (causal convs never look right, so nothing else
   reads those rows).
 * The ELU in front of every encoder conv is applied to the GEMM's A operand as it is loaded (QT_AACT_ELU).
-* Nearest-codeword search: one block per frame, all codewords scored in fp32 (qt_rvq_encode).
+* Nearest-codeword search: per codebook stage one launch over (codeword slice x frame tile) blocks, exact fp32
+  distances, deterministic last-arriver reduction (qt_rvq_encode).
 """
 from __future__ import annotations
 

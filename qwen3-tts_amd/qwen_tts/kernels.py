@@ -321,9 +321,13 @@ def layernorm(x, w, b, eps, out, M, N, ldx=None, ldo=None):
                                   ldo or N, M, N, stream()), "qt_layernorm")
 
 
-def rvq_encode(x, ldx, tab, tabT, Q, cb, D, R, codes, codes_ld):
-    check(_hip.lib().qt_rvq_encode(ptr(x), ldx, ptr(tab), ptr(tabT), Q, cb, D, R, ptr(codes), codes_ld, stream()),
-          "qt_rvq_encode")
+def rvq_encode(x, ldx, tab, tabT, Q, cb, D, R, codes, codes_ld, ws=None):
+    """ws: zero-initialised uint8 device scratch (reusable; allocated here when None)."""
+    need = int(_hip.lib().qt_rvq_encode_ws_bytes(R, D, cb))
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(max(need, 1), dtype=torch.uint8, device=x.device)
+    check(_hip.lib().qt_rvq_encode(ptr(x), ldx, ptr(tab), ptr(tabT), Q, cb, D, R, ptr(codes), codes_ld, ptr(ws),
+                                   ws.numel(), stream()), "qt_rvq_encode")
 
 
 def mel_logmag(spec, ld_spec, F_, nbin, basis, nmel, out, ldo=None):

@@ -147,7 +147,7 @@ def test_polyphase_strided_conv(r, C, L):
     torch.testing.assert_close(out.view(B, Tn, 2 * C)[:, :nv].cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("D,cb,Q,R", [(32, 2048, 15, 21), (256, 2048, 3, 8), (24, 300, 4, 5)])
+@pytest.mark.parametrize("D,cb,Q,R", [(32, 2048, 15, 21), (256, 2048, 3, 8), (24, 320, 4, 5), (256, 2048, 2, 77)])
 def test_rvq_encode_nearest_codeword(D, cb, Q, R):
     from qwen_tts import kernels as Kn
     dev = _dev()
