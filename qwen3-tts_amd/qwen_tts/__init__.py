@@ -6,7 +6,9 @@ HIP kernels); there is no CPU fallback.
 """
 __version__ = "0.0.4+mi355x"
 
-from .inference.qwen3_tts_model import Qwen3TTSModel, VoiceClonePromptItem  # noqa: E402,F401
+from .inference.qwen3_tts_model import (Qwen3TTSModel, VoiceClonePromptItem, load_voice_clone_prompt,  # noqa: E402,F401
+                                       save_voice_clone_prompt)
 from .inference.qwen3_tts_tokenizer import Qwen3TTSTokenizer  # noqa: E402,F401
 
-__all__ = ["__version__", "Qwen3TTSModel", "Qwen3TTSTokenizer", "VoiceClonePromptItem"]
+__all__ = ["__version__", "Qwen3TTSModel", "Qwen3TTSTokenizer", "VoiceClonePromptItem", "load_voice_clone_prompt",
+           "save_voice_clone_prompt"]

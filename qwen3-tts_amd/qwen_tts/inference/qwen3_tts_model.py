@@ -38,6 +38,47 @@ class VoiceClonePromptItem:
     ref_text: Optional[str] = None
 
 
+def save_voice_clone_prompt(items: List[VoiceClonePromptItem], path: str) -> None:
+    """The reference demo's voice file (qwen_tts/cli/demo.py:514-521): torch.save({"items": [asdict(item)]}),
+    tensors moved to the CPU so the file loads anywhere."""
+    from dataclasses import asdict
+    out = []
+    for it in items:
+        d = asdict(it)
+        for k in ("ref_code", "ref_spk_embedding"):
+            if isinstance(d[k], torch.Tensor):
+                d[k] = d[k].detach().cpu()
+        out.append(d)
+    torch.save({"items": out}, path)
+
+
+def load_voice_clone_prompt(path: str) -> List[VoiceClonePromptItem]:
+    """Read a voice file written by save_voice_clone_prompt or the reference demo (demo.py:527-563), with
+    torch.load(weights_only=True) like the reference: no code in the file is executed."""
+    payload = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(payload, dict) or "items" not in payload:
+        raise ValueError("Invalid file format")
+    raw = payload["items"]
+    if not isinstance(raw, list) or len(raw) == 0:
+        raise ValueError("Empty voice items")
+    items = []
+    for d in raw:
+        if not isinstance(d, dict):
+            raise ValueError("Invalid item format in file")
+        ref_code = d.get("ref_code", None)
+        if ref_code is not None and not torch.is_tensor(ref_code):
+            ref_code = torch.tensor(ref_code)
+        spk = d.get("ref_spk_embedding", None)
+        if spk is None:
+            raise ValueError("Missing ref_spk_embedding")
+        if not torch.is_tensor(spk):
+            spk = torch.tensor(spk)
+        xv = bool(d.get("x_vector_only_mode", False))
+        items.append(VoiceClonePromptItem(ref_code=ref_code, ref_spk_embedding=spk, x_vector_only_mode=xv,
+                                          icl_mode=bool(d.get("icl_mode", not xv)), ref_text=d.get("ref_text", None)))
+    return items
+
+
 class Qwen3TTSModel:
     def __init__(self, model: TTSModel, processor, generate_defaults: Optional[Dict[str, Any]] = None):
         self.model = model

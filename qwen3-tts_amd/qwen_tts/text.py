@@ -41,6 +41,22 @@ class FallbackProcessor:
 
 
 def load_processor(path: str):
+    """The checkpoint's Qwen2 BPE tokenizer when its files are present (the reference loads it through
+    AutoProcessor, W:103-108): `tokenizer_config.json` + `vocab.json` / `merges.txt` (or `tokenizer.json`) via
+    transformers' AutoTokenizer from the local directory; a bare `tokenizer.json` via the `tokenizers` library;
+    otherwise the deterministic stand-in above."""
+    if os.path.exists(os.path.join(path, "tokenizer_config.json")) and (
+            os.path.exists(os.path.join(path, "vocab.json")) or os.path.exists(os.path.join(path, "tokenizer.json"))):
+        from transformers import AutoTokenizer
+        hf = AutoTokenizer.from_pretrained(path, local_files_only=True)
+
+        class _HF:
+            tokenizer = hf
+
+            def __call__(self, text, return_tensors="pt", padding=True):
+                return {"input_ids": torch.tensor([hf(text)["input_ids"]], dtype=torch.long)}
+
+        return _HF()
     tj = os.path.join(path, "tokenizer.json")
     if os.path.exists(tj):
         from tokenizers import Tokenizer

@@ -357,6 +357,18 @@ def test_voice_clone_prompt_and_generate(tiny_base):
                                      ref_text="a reference transcript", **kw)
     assert sr == 24000 and len(wa) == 1
     np.testing.assert_array_equal(wa[0], wb[0])
+    # the reference demo's voice file ({"items": [asdict(item)]}, torch.save / torch.load(weights_only=True))
+    import tempfile
+    from qwen_tts import load_voice_clone_prompt, save_voice_clone_prompt
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "voice.pt")
+        save_voice_clone_prompt(items, path)
+        raw = torch.load(path, map_location="cpu", weights_only=True)
+        assert set(raw["items"][0]) == {"ref_code", "ref_spk_embedding", "x_vector_only_mode", "icl_mode", "ref_text"}
+        loaded = load_voice_clone_prompt(path)
+    assert loaded[0].ref_text == "a reference transcript" and loaded[0].icl_mode
+    wl, _ = tts.generate_voice_clone("hello there", language="English", voice_clone_prompt=loaded, **kw)
+    np.testing.assert_array_equal(wa[0], wl[0])
     xv = tts.create_voice_clone_prompt((w, 24000), x_vector_only_mode=True)
     assert xv[0].ref_code is None and xv[0].x_vector_only_mode
     wc, _ = tts.generate_voice_clone("hello there", language="English", voice_clone_prompt=xv, **kw)
