@@ -243,6 +243,8 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
         wv[u] = __builtin_nontemporal_load((const u32x4_t*)(wp + (size_t)kc * 64 * E));
       else
         wv[u] = *(const u32x4_t*)(wp + (size_t)kc * 64 * E);
+      // every lane loads (rows >= M re-fetch row M-1 from L2): predicating the load on the row was measured
+      // slower (profiles/r01_gemv_variants_ab.jsonl)
       if constexpr (E == 8) load8f(arow + kc * KT, a[u]); else load4f(arow + kc * KT, a[u]);
     }
 #pragma unroll
@@ -584,10 +586,14 @@ void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
   }
 }
 
-// U = k tiles in flight per wave: 8 when a wave owns 5..8 (one round trip instead of two; measured slower at 12)
+// U = k tiles in flight per wave: 8 when a wave owns 5..8 (one round trip instead of two).  Forcing U = 8 on
+// every shape, or 16, was measured slower (register pressure; profiles/r01_gemv_variants_ab.jsonl).
+// QT_GEMV_U (4 / 8) overrides for A/B measurement.
 template <typename WT, typename AT, typename OT, int WPB>
 void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
-  if (per > 4 && per <= 8) launch_gemv_u<WT, AT, OT, WPB, 8>(p, nt, s);
+  static const int u_env = [] { const char* e = getenv("QT_GEMV_U"); return e ? atoi(e) : 0; }();
+  const int u = u_env ? u_env : ((per > 4 && per <= 8) ? 8 : 4);
+  if (u >= 8) launch_gemv_u<WT, AT, OT, WPB, 8>(p, nt, s);
   else launch_gemv_u<WT, AT, OT, WPB, 4>(p, nt, s);
 }
 
