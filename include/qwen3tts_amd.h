@@ -143,6 +143,29 @@ int qt_decode_attention(const qt_decode_attn_args* args, void* stream);
 int qt_small_prefill_attention(const qt_decode_attn_args* args, int T, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * qt_decode_attn_oproj: qt_decode_attention + the o_proj GEMV + residual add in one launch, for short caches
+ * (the code predictor's decode steps, M:930-958 attention -> o_proj -> M:1004 residual):
+ *   x[r][n] += sum_k Wo[n][k] * attn(r)[k],  attn as qt_decode_attention computes it (rounded to the weight
+ *   dtype, as the separate path stores it before the o_proj MFMA).
+ * Row r is batch entry r; keys [row_start[r], kv_pos[r]] (or [0, const_pos] when const_pos >= 0); Hkv <= 8.
+ * w_o: o_proj weight tiled by qt_tile_weight ([N][Hq*D], w_dtype == kv_dtype).  x: fp32 residual [R][ldx].
+ * One block per (column group, row) recomputes the row's attention for every kv head and sums the per-head
+ * partial products in head order inside the block (deterministic, no workspace).  Each block re-reads its
+ * row's keys, so use it where keys are few (<= 64 cached keys).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_attn_oproj_args {
+  int R, Hq, Hkv, D, Lmax;
+  const float* qkv;                       /* fp32 [R][(Hq + 2*Hkv)*D] raw q/k/v projections */
+  const float* q_norm; const float* k_norm; float eps;
+  const float* cos_tab; const float* sin_tab;
+  const int* rope_pos; const int* kv_pos; const int* row_start; int const_pos;
+  void* k_cache; void* v_cache; int kv_dtype;
+  const void* w_o; int w_dtype; int N;
+  float* x; long long ldx;
+} qt_attn_oproj_args;
+int qt_decode_attn_oproj(const qt_attn_oproj_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * qt_mlp_decode: one decode step of the Qwen3 MLP with its residual, fused (M:655-668: down_proj(act(gate_proj
  * (x)) * up_proj(x)) after the post-attention RMSNorm, + residual): x[m] += W_down(silu(W_gate n(x)) * W_up n(x)).
  * M <= 16 rows (fp32 residual x, row stride ldx), H in {1024, 2048}, I % 32 == 0, H/16 <= I/32 <= 256;

@@ -67,6 +67,40 @@ QT_DEV float group_sum_dpp(float v) {
   return v;
 }
 
+// Lane exchange with lane ^ OFF.  OFF = 16 / 32 use the gfx950 VALU permlane swaps (v_permlane{16,32}_swap_b32:
+// no LDS round trip, unlike ds_bpermute); OFF = 1 / 2 quad DPP, 8 row_ror:8 within a 16-lane row; else ds_bpermute.
+template <int OFF>
+QT_DEV float xor_lane(float v) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (OFF == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float((lane & 32) ? r[0] : r[1]);
+  } else if constexpr (OFF == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float((lane & 16) ? r[0] : r[1]);
+  } else if constexpr (OFF == 1) {
+    return dpp_f<0xB1>(v);  // quad_perm [1,0,3,2]
+  } else if constexpr (OFF == 2) {
+    return dpp_f<0x4E>(v);  // quad_perm [2,3,0,1]
+  } else {
+    return __shfl_xor(v, OFF, 64);
+  }
+}
+// Partner of a lane in the other half of an aligned group of N lanes (lane ^ N/2): rotate-half RoPE pairs
+template <int N>
+QT_DEV float half_partner(float v) {
+  if constexpr (N == 16) return dpp_f<0x128>(v);  // row_ror:8
+  else return xor_lane<N / 2>(v);
+}
+// Full-wave float sum, wave-uniform result: DPP inside rows, then the four row sums by readlane
+QT_DEV float wave_sum_dpp(float v) {
+  v = group_sum_dpp<16>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+}
+
 QT_DEV float silu_f(float g) { return g / (1.0f + expf(-g)); }
 QT_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 QT_DEV float elu_f(float x) { return x > 0.f ? x : expm1f(x); }

@@ -60,6 +60,14 @@ class DecodeAttnArgs(ctypes.Structure):
                 ("ws", c_void_p), ("ws_bytes", c_ll)]
 
 
+class AttnOprojArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("Hq", c_int), ("Hkv", c_int), ("D", c_int), ("Lmax", c_int), ("qkv", c_void_p),
+                ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float), ("cos_tab", c_void_p), ("sin_tab", c_void_p),
+                ("rope_pos", c_void_p), ("kv_pos", c_void_p), ("row_start", c_void_p), ("const_pos", c_int),
+                ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int), ("w_o", c_void_p), ("w_dtype", c_int),
+                ("N", c_int), ("x", c_void_p), ("ldx", c_ll)]
+
+
 class SampleArgs(ctypes.Structure):
     _fields_ = [("logits", c_void_p), ("R", c_int), ("V", c_int), ("ld", c_ll), ("seen", c_void_p),
                 ("rep_penalty", c_float), ("n_generated", c_void_p), ("min_new_tokens", c_int), ("eos_id", c_int),
@@ -78,6 +86,7 @@ class MlpArgs(ctypes.Structure):
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
+           "qt_decode_attn_oproj",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -107,6 +116,7 @@ def load_library(path: str = LIB_PATH):
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
         "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
+        "qt_decode_attn_oproj": [P, P],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],

@@ -235,6 +235,20 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
     check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
 
 
+def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc, Lmax, w_o: "Tiled", x, *,
+                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None):
+    """qt_decode_attn_oproj: x[:R] += o_proj(decode attention) in one launch (row r = batch entry r, short caches)."""
+    a = _hip.AttnOprojArgs()
+    a.R, a.Hq, a.Hkv, a.D, a.Lmax = R, Hq, Hkv, D, Lmax
+    a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    a.rope_pos, a.kv_pos, a.row_start, a.const_pos = ptr(rope_pos), ptr(kv_pos), ptr(row_start), const_pos
+    a.k_cache, a.v_cache, a.kv_dtype = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype)
+    a.w_o, a.w_dtype, a.N = ptr(w_o.w), _hip.dtype_code(w_o.dtype), w_o.N
+    a.x, a.ldx = ptr(x), x.stride(0)
+    check(_hip.lib().qt_decode_attn_oproj(ctypes.byref(a), stream()), "qt_decode_attn_oproj")
+
+
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,

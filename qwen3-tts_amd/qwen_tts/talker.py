@@ -66,10 +66,15 @@ class _Stack:
     def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False):
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
         decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention."""
+        # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
+        fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
             K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
-            if decode:
+            if fused_ao:
+                K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
+                                    self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"])
+            elif decode:
                 K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                    self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
                                    meta["row_start"], kc, vc, Lmax, scratch["att"], const_pos=meta.get("const_pos", -1))
@@ -81,7 +86,8 @@ class _Stack:
                            self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
                 K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
-            K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
+            if not fused_ao:
+                K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
             if "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
                 K.mlp_decode(x, R, self.H, self.I, L.gu, L.down, self.eps, scratch["mlp_ws"], scratch["mlp_err"])
             else:
@@ -93,19 +99,30 @@ class _Stack:
 # (CP 17.1 vs 14.6 us, talker 31.6 vs 22.8 us: its 96-192 blocks stream the weights through fewer CUs and the
 # cross-block reduction adds ~3 dependent round trips), so it is opt-in.
 FUSED_MLP = os.environ.get("QT_FUSED_MLP", "0") == "1"
+# code-predictor decode steps: qt_decode_attn_oproj (attention fused into o_proj + residual); QT_ATTN_OPROJ=0 keeps
+# the two-launch path (decode attention, then the o_proj GEMV) for A/B measurement
+ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 
 
-def _scratch(R, st: _Stack, dev):
+def _scratch(R, st: _Stack, dev, attn_oproj=False):
     """Per-forward activations.  The attention output and the SwiGLU output only feed the next GEMM's MFMA,
     which rounds its A operand to the weight dtype anyway: in bf16 mode they are stored as bf16 (same RNE
     rounding, half the bytes the o_proj / down GEMVs read)."""
     f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
     a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
     sc = {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
+    sc["attn_oproj"] = attn_oproj and ATTN_OPROJ and _attn_oproj_ok(st)
     if FUSED_MLP and R <= 16 and K.mlp_supported(st.H, st.I, st.wdt):  # fused decode MLP scratch
         sc["mlp_ws"] = torch.zeros(K.mlp_ws_bytes(R, st.H, st.I), dtype=torch.uint8, device=dev)
         sc["mlp_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
     return sc
+
+
+def _attn_oproj_ok(st: _Stack) -> bool:
+    kt = 32 if st.wdt == torch.bfloat16 else 16
+    ks = (st.Hq // st.Hkv) * st.D
+    return (st.D in (16, 64, 128) and st.Hq // st.Hkv in (1, 2, 4) and st.Hkv <= 8 and ks % kt == 0
+            and ks // kt <= 16)
 
 
 @dataclass
@@ -168,7 +185,7 @@ class Session:
         self.cp_x = f32(2 * B, c.H)
         self.cp_logits = f32(B, eng.Vc)
         self.sc_t = _scratch(B, t, dev)
-        self.sc_c = _scratch(2 * B, c, dev)
+        self.sc_c = _scratch(2 * B, c, dev, attn_oproj=True)
         self.codes = i32(B, max_frames + 2, self.G)
         self.hiddens = f32(B, max_frames + 1, t.H)
         self.tok0 = i32(B)

@@ -357,6 +357,64 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
         torch.testing.assert_close(outs[0], a2, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("D,hq,hkv,L,N,B", [(128, 16, 8, 17, 1024, 8), (128, 16, 8, 3, 1024, 16), (128, 8, 4, 40, 200, 3),
+                                            (16, 8, 2, 9, 32, 5), (64, 4, 4, 64, 96, 1)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_decode_attn_oproj_matches_two_kernel_path(D, hq, hkv, L, N, B, dt):
+    """qt_decode_attn_oproj (attention fused into o_proj + residual, head partials summed in-block) == qt_decode_attention
+    followed by the o_proj GEMV with residual add; same cache writes; bitwise reproducible; const_pos == arrays."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(L * 7 + D + N)
+    qkv = torch.randn(B, (hq + 2 * hkv) * D, generator=g).to(dev)
+    qn, kn = (1 + 0.1 * torch.randn(D, generator=g)).to(dev), (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    Lmax = L + 2
+    kc = torch.randn(B, hkv, Lmax, D, generator=g).to(dev, dt)
+    vc = torch.randn(B, hkv, Lmax, D, generator=g).to(dev, dt)
+    Wo = torch.randn(N, hq * D, generator=g) * 0.05
+    wo = Kn.tile_linear(Wo.to(dev), dt)
+    x0 = torch.randn(B, N, generator=g).to(dev)
+    cos, sin = Kn.rope_tables(D, 1e6, Lmax + 8, dev)
+    i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
+    pos = i32([L - 1] * B)
+    rb, zero = i32(range(B)), i32([0] * B)
+    # two-kernel reference
+    kc1, vc1 = kc.clone(), vc.clone()
+    att = torch.zeros(B, hq * D, device=dev, dtype=dt)
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, pos, zero, kc1, vc1, Lmax, att)
+    x1 = x0.clone()
+    Kn.gemm(att, wo, x1, B, hq * D, N, epi=_hip.EPI_ADD, splitk=1)
+    outs = []
+    for _ in range(2):
+        kc2, vc2 = kc.clone(), vc.clone()
+        x2 = x0.clone()
+        Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc2, vc2, Lmax, wo, x2, const_pos=L - 1)
+        ktol = 2e-6 if dt == torch.float32 else 1e-2  # fp contraction of the k RMSNorm + RoPE / one bf16 ulp
+        torch.testing.assert_close(kc2.float(), kc1.float(), atol=ktol, rtol=ktol)
+        assert torch.equal(vc2, vc1)
+        outs.append(x2)
+    assert torch.equal(outs[0], outs[1])
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    torch.testing.assert_close(outs[0], x1, atol=tol, rtol=tol)
+    # the same positions through device arrays (rope_pos / kv_pos / row_start) give the same bits
+    kc3, vc3 = kc.clone(), vc.clone()
+    x3 = x0.clone()
+    Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc3, vc3, Lmax, wo, x3,
+                         rope_pos=pos, kv_pos=pos, row_start=zero)
+    assert torch.equal(x3, outs[0]) and torch.equal(kc3, kc2)
+    # ragged key ranges (row_start > 0) through the arrays path vs the two-kernel path
+    start = i32([(b * 3) % max(L - 1, 1) for b in range(B)])
+    kc4, vc4, kc5, vc5 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    att4 = torch.zeros(B, hq * D, device=dev, dtype=dt)
+    Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, pos, rb, pos, start, kc4, vc4, Lmax, att4)
+    x4 = x0.clone()
+    Kn.gemm(att4, wo, x4, B, hq * D, N, epi=_hip.EPI_ADD, splitk=1)
+    x5 = x0.clone()
+    Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc5, vc5, Lmax, wo, x5,
+                         rope_pos=pos, kv_pos=pos, row_start=start)
+    torch.testing.assert_close(x5, x4, atol=tol, rtol=tol)
+
+
 @pytest.mark.parametrize("D,hq,hkv", [(128, 16, 8), (16, 4, 2), (64, 4, 4)])
 @pytest.mark.parametrize("kvdt", [torch.float32, torch.bfloat16])
 def test_small_prefill_attention_matches_two_kernel_path(D, hq, hkv, kvdt):
