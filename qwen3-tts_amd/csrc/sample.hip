@@ -8,6 +8,7 @@
 // per-thread masses), so it is an exact sample of the warped distribution; RNG streams differ from
 // torch.multinomial, hence parity is distribution-level (tests/test_gpu_parity.py).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -54,8 +55,14 @@ QT_DEV float block_max(float v, float* sh) {
   return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
 }
 
+struct SK {
+  qt_sample_args a;
+  int stop;  // measurement hook (QT_SAMPLE_STOP): end after phase 1..5; 0 = the full kernel
+};
+
 template <int PER>
-__global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
+__global__ __launch_bounds__(NT) void sample_k(SK pk) {
+  const qt_sample_args& p = pk.a;
   __shared__ float sh[8];
   __shared__ int shi[4];
   __shared__ int cnt3[2][2][4];
@@ -80,6 +87,10 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
       if (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) x = -INFINITY;
     }
     s[j] = x;
+  }
+  if (pk.stop == 1) {
+    if (s[0] + s[PER - 1] == 1234.5f) p.tok_out[r] = 0;
+    return;
   }
   int tok;
   if (!p.do_sample) {
@@ -108,6 +119,10 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) { s[j] *= invT; mx = fmaxf(mx, s[j]); }
     mx = block_max(mx, sh);
+    if (pk.stop == 2) {
+      if (mx == 1234.5f) p.tok_out[r] = 0;
+      return;
+    }
     unsigned tk = 0;  // keep keys >= tk
     if (p.top_k > 0 && p.top_k < V) {
       unsigned key[PER];
@@ -169,6 +184,10 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
         tk = shtk;
       }
     }
+    if (pk.stop == 3) {
+      if (tk == 12345u) p.tok_out[r] = 0;
+      return;
+    }
     if (p.top_p < 1.0f) {  // rare path: sorted list (descending) for the nucleus cut
       for (int j = 0; j < PER; ++j) {
         const int v = tid + j * NT;
@@ -224,6 +243,10 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
     for (int i = 0; i < w; ++i) off += sh[i];
     const float total = sh[0] + sh[1] + sh[2] + sh[3];
     inc += off;
+    if (pk.stop == 4) {
+      if (inc == 1234.5f) p.tok_out[r] = 0;
+      return;
+    }
     const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)(p.row_base + r)) * total;
     const float excl = inc - mass;
     if (tid == 0) shi[0] = -1;
@@ -248,6 +271,10 @@ __global__ __launch_bounds__(NT) void sample_k(qt_sample_args p) {
     }
   }
   if (fin) tok = p.eos_id;
+  if (pk.stop == 5) {
+    if (tid == 0) p.tok_out[r] = tok;
+    return;
+  }
   if (p.emb_table) {  // next-step input row: the chosen token's (projected) embedding
     const float* src = p.emb_table + (long long)tok * p.emb_dim;
     float* dst = p.emb_out + (long long)r * p.emb_ld;
@@ -270,8 +297,10 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  if (a->V <= NT * 8) hipLaunchKernelGGL(sample_k<8>, dim3(a->R), dim3(NT), 0, st, *a);
-  else if (a->V <= NT * 12) hipLaunchKernelGGL(sample_k<12>, dim3(a->R), dim3(NT), 0, st, *a);
-  else hipLaunchKernelGGL(sample_k<16>, dim3(a->R), dim3(NT), 0, st, *a);
+  static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
+  const SK k{*a, stop};
+  if (a->V <= NT * 8) hipLaunchKernelGGL(sample_k<8>, dim3(a->R), dim3(NT), 0, st, k);
+  else if (a->V <= NT * 12) hipLaunchKernelGGL(sample_k<12>, dim3(a->R), dim3(NT), 0, st, k);
+  else hipLaunchKernelGGL(sample_k<16>, dim3(a->R), dim3(NT), 0, st, k);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }
