@@ -342,11 +342,24 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     const float* base = p.part + (size_t)nt * p.ks * PS;
 #pragma unroll
     for (int i = 0; i < 4; ++i) { v[i] = 0.f; ssr[i] = 0.f; }
-    for (int s = 0; s < p.ks; ++s) {
+    // four splits' partials in flight before their adds (a dependent add per split would serialise the round trips)
+    for (int s0 = 0; s0 < p.ks; s0 += 4) {
+      float pv[4][4], ps[4][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] += __hip_atomic_load(base + s * PS + lane * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (NORM) ssr[i] += __hip_atomic_load(base + s * PS + 256 + lk * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int s = 0; s < 4; ++s) {
+        const int sc = min(s0 + s, p.ks - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pv[s][i] = __hip_atomic_load(base + sc * PS + lane * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ps[s][i] = NORM ? __hip_atomic_load(base + sc * PS + 256 + lk * 4 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s0 + s < p.ks) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { v[i] += pv[s][i]; ssr[i] += ps[s][i]; }
+        }
       }
     }
   }
@@ -902,11 +915,13 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   const bool lds_auto = lds_env && a->w_dtype == QT_BF16 && a->splitk == 0;  // gemv_lds replaces auto split-K
   if (a->M <= 16 && a->taps == 0 && a->K % KT == 0 && a->gamma == nullptr && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN &&
       a->splitk != 1 && ntl <= 4096 && !lds_auto) {
-    // auto: split only deep-K shapes on < 256 column tiles (measured: the ~2 us arrival/reduce cost pays
-    // only when it removes a second weight round trip; down-proj with bf16 activations: 2048x6144 10.1 ->
-    // 9.8 us, 1024x3072 7.4 -> 7.1 us at split 2, split 4 slower)
+    // auto: split only deep-K shapes on < 256 column tiles (the arrival / partial round trips pay only when they
+    // remove weight round trips).  Measured cold, paired-A GEMV, partial loads of four splits in flight:
+    // 2048x6144 11.4 (no split) / 10.9 (2) / 10.3 us (4), 1024x3072 8.5 / 7.6 / 7.1 us; other shapes lose.
+    // In the frame graph split 2 wins (bench 158.6 vs 157.2 audio-s/s, same box): QT_GEMV_SPLIT_AUTO overrides
     const int wpb1 = ktl >= 48 ? 16 : (ktl >= 16 ? 8 : 4), per1 = (ktl + wpb1 - 1) / wpb1;
-    int ks = a->splitk > 1 ? a->splitk : ((per1 > 4 && ntl < 256) ? 2 : 1);  // bf16-A down-proj: 2 best
+    static const int ks_auto = [] { const char* e = getenv("QT_GEMV_SPLIT_AUTO"); return e ? atoi(e) : 2; }();
+    int ks = a->splitk > 1 ? a->splitk : ((per1 > 4 && ntl < 256) ? ks_auto : 1);
     ks = std::max(1, std::min({ks, 16, ktl / 2}));
     const size_t need = 4096 * sizeof(unsigned) + (size_t)ntl * ks * (64 * 4 + 16) * sizeof(float);
     if (ks > 1 && need <= (size_t)a->ws_bytes) {
