@@ -10,6 +10,89 @@
 
 namespace {
 
+// v_exp_f32 without the library's denormal-range scaling: arguments here are score differences <= 0, where
+// results below 2^-126 (flushed) weigh nothing next to the row maximum's 1
+QT_DEV float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Merge the online-softmax states (m, l, o[NREP][8]) of the lane groups of one wave (LPK lanes per group, each
+// group's m uniform inside it): common max over the groups (readlane), rescale, then plain sums over the groups.
+// Result: lane `lane` owns `cnt` consecutive output values starting at dim `d0` of head `jh` (totals of o) and
+// that head's total l.  LPK == 16, NREP == 2 (the Qwen3 heads): a transpose-reduce over the four 16-lane rows
+// -- two values share each VALU permlane swap, 12 swaps + 12 adds for the 16 o sums, every lane owns 4 outputs.
+// Other shapes: xor butterflies, lane group 0 owns 8 outputs per head (cnt = 8 per head, looped by the caller).
+template <int LPK, int NREP>
+struct GroupMerge {
+  static constexpr bool TR = LPK == 16 && NREP == 2;
+  float mm[NREP];  // common max per head
+  float t[TR ? 4 : NREP * 8];
+  float lt[TR ? 1 : NREP];
+  QT_DEV void run(float (&m)[NREP], float (&l)[NREP], float (&o)[NREP][8]) {
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m[j]), 0));
+#pragma unroll
+      for (int g2 = LPK; g2 < 64; g2 += LPK)
+        x = fmaxf(x, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m[j]), g2)));
+      mm[j] = x;
+      const float f = (m[j] == -INFINITY || x == -INFINITY) ? 0.f : exp2_hw(m[j] - x);
+      l[j] *= f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[j][i] *= f;
+    }
+    if constexpr (TR) {
+      float v[16], s8[8];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = o[i >> 3][i & 7];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // rows 0-1: v[i] half sums, rows 2-3: v[i + 8]
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+        s8[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // row rho: total of v[i + 4 rho]
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s8[i]), __float_as_uint(s8[i + 4]), false, false);
+        t[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      const auto rl = __builtin_amdgcn_permlane32_swap(__float_as_uint(l[0]), __float_as_uint(l[1]), false, false);
+      const float lh = __uint_as_float(rl[0]) + __uint_as_float(rl[1]);
+      const auto rl2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(lh), __float_as_uint(lh), false, false);
+      lt[0] = __uint_as_float(rl2[0]) + __uint_as_float(rl2[1]);  // rows 0-1: l[0], rows 2-3: l[1]
+    } else {
+      auto gsum = [](float x) {
+        if constexpr (LPK <= 1) x += xor_lane<1>(x);
+        if constexpr (LPK <= 2) x += xor_lane<2>(x);
+        if constexpr (LPK <= 4) x += xor_lane<4>(x);
+        if constexpr (LPK <= 8) x += xor_lane<8>(x);
+        if constexpr (LPK <= 16) x += xor_lane<16>(x);
+        x += xor_lane<32>(x);
+        return x;
+      };
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        lt[j] = gsum(l[j]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[j * 8 + i] = gsum(o[j][i]);
+      }
+    }
+  }
+  // visit (head, dim, total o, head total l, head max) for the outputs this lane owns
+  template <typename F>
+  QT_DEV void each(int lane, F&& f) const {
+    const int sub = lane % LPK;
+    if constexpr (TR) {
+      const int rho = lane >> 4, jh = rho >> 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f(jh, sub * 8 + 4 * (rho & 1) + i, t[i], lt[0], mm[jh]);
+    } else {
+      if (lane / LPK != 0) return;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f(j, sub * 8 + i, t[j * 8 + i], lt[j], mm[j]);
+    }
+  }
+};
+
 template <typename KV>
 __global__ __launch_bounds__(64) void qkv_post_k(qt_qkv_args p) {
   const int r = blockIdx.x, hh = blockIdx.y, lane = threadIdx.x;
@@ -333,10 +416,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
 #pragma unroll
       for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
       if (mn == -INFINITY) continue;  // no valid key yet in this lane group
-      const float f = exp2f(m[j] - mn);
+      const float f = exp2_hw(m[j] - mn);
       float e[IC], es = 0.f;
 #pragma unroll
-      for (int c = 0; c < IC; ++c) { e[c] = exp2f(dd[j][c] - mn); es += e[c]; }
+      for (int c = 0; c < IC; ++c) { e[c] = exp2_hw(dd[j][c] - mn); es += e[c]; }
       l[j] = l[j] * f + es;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -356,15 +439,16 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
     if (j0 + 2 * GIC < j_hi) load_into(j0 + 2 * GIC, kr, vr);
     consume(kn, vn, j0 + GIC);
   }
-  // merge lane groups inside the wave
+  // merge lane groups inside the wave (ds_bpermute butterflies: the permlane transpose-reduce GroupMerge was
+  // measured 3 us slower in this kernel, 11.3 vs 8.2 us at 210 keys, tools/talker_attn_bench.py)
 #pragma unroll
   for (int off = LPK; off < 64; off <<= 1) {
 #pragma unroll
     for (int j = 0; j < NREP; ++j) {
       const float m2 = __shfl_xor(m[j], off, 64), l2 = __shfl_xor(l[j], off, 64);
       const float mn = fmaxf(m[j], m2);
-      const float f1 = m[j] == -INFINITY ? 0.f : exp2f(m[j] - mn);
-      const float f2 = m2 == -INFINITY ? 0.f : exp2f(m2 - mn);
+      const float f1 = m[j] == -INFINITY ? 0.f : exp2_hw(m[j] - mn);
+      const float f2 = m2 == -INFINITY ? 0.f : exp2_hw(m2 - mn);
       l[j] = l[j] * f1 + l2 * f2;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -393,7 +477,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
     float ll = 0.f, oo = 0.f;
     for (int ww = 0; ww < NW; ++ww) {
       const float mw = mrg_ml[ww][j][0];
-      const float f = mw == -INFINITY ? 0.f : exp2f(mw - mm);
+      const float f = mw == -INFINITY ? 0.f : exp2_hw(mw - mm);
       ll += mrg_ml[ww][j][1] * f;
       oo += mrg_o[ww][j][d] * f;
     }
@@ -434,7 +518,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
     for (int zz = 0; zz < nsplit; ++zz) mm = fmaxf(mm, ms[zz]);
     float ll = 0.f, oo = 0.f;
     for (int zz = 0; zz < nsplit; ++zz) {
-      const float f = ms[zz] == -INFINITY ? 0.f : exp2f(ms[zz] - mm);
+      const float f = ms[zz] == -INFINITY ? 0.f : exp2_hw(ms[zz] - mm);
       ll += ls[zz] * f;
       oo += os[zz] * f;
     }
@@ -533,10 +617,6 @@ __global__ __launch_bounds__(64 * T * (NREP + 2)) void attn_small_prefill_k(qt_d
 // model dims) so the weight slice is fetched into one L2 and re-read by the R row blocks.  Block cg == 0 appends
 // the new k/v to the cache.  Re-reading a row's keys per column group costs R x CG x keys x 2 x D x sizeof(kv) of
 // L2 / MALL reads: cheap for the code predictor's <= 17 keys, too much for the talker's long caches.
-// v_exp_f32 without the library's denormal-range scaling: arguments here are score differences <= 0, where
-// results below 2^-126 (flushed) weigh nothing next to the row maximum's 1
-QT_DEV float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
-
 struct AOK {
   qt_attn_oproj_args a;
   int stop;  // measurement hook (QT_AO_STOP): end after phase 1..4; 0 = the full kernel
@@ -751,61 +831,9 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < NREP; ++j) {  // common max (a group's m is uniform inside it), rescale
-      float mm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m[j]), 0));
-#pragma unroll
-      for (int g2 = LPK; g2 < 64; g2 += LPK)
-        mm = fmaxf(mm, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m[j]), g2)));
-      const float f = m[j] == -INFINITY ? 0.f : exp2_hw(m[j] - mm);
-      l[j] *= f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[j][i] *= f;
-    }
-    if constexpr (LPK == 16 && NREP == 2) {
-      // transpose-reduce over the 4 lane groups (rows): two values share one permlane swap, so the 16 o sums
-      // take 12 swaps + 12 adds; afterwards row rho holds the totals of o[rho / 2][4 (rho % 2) .. + 4]
-      float v[16], s8[8], t4[4];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = o[i >> 3][i & 7];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
-        s8[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows 0-1: v[i] half sums, rows 2-3: v[i+8]
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s8[i]), __float_as_uint(s8[i + 4]), false, false);
-        t4[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // row rho: total of v[i + 4 rho]
-      }
-      const auto rl = __builtin_amdgcn_permlane32_swap(__float_as_uint(l[0]), __float_as_uint(l[1]), false, false);
-      const float lh = __uint_as_float(rl[0]) + __uint_as_float(rl[1]);
-      const auto rl2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(lh), __float_as_uint(lh), false, false);
-      const float inv = 1.f / (__uint_as_float(rl2[0]) + __uint_as_float(rl2[1]));  // rows 0-1: l[0], rows 2-3: l[1]
-      const int rho = lane >> 4;
-      AT* dst = &att[w][(rho >> 1) * D + sub * 8 + 4 * (rho & 1)];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dst[i] = from_f<AT>(t4[i] * inv);
-    } else {
-      auto gsum = [&](float v) {  // sum over the lane groups (lanes with equal sub)
-        if constexpr (LPK <= 1) v += xor_lane<1>(v);
-        if constexpr (LPK <= 2) v += xor_lane<2>(v);
-        if constexpr (LPK <= 4) v += xor_lane<4>(v);
-        if constexpr (LPK <= 8) v += xor_lane<8>(v);
-        if constexpr (LPK <= 16) v += xor_lane<16>(v);
-        v += xor_lane<32>(v);
-        return v;
-      };
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        const float inv = 1.f / gsum(l[j]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float ov = gsum(o[j][i]) * inv;
-          if (grp == 0) att[w][j * D + sub * 8 + i] = from_f<AT>(ov);
-        }
-      }
-    }
+    GroupMerge<LPK, NREP> gm;
+    gm.run(m, l, o);
+    gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = from_f<AT>(ov / lv); });
   }
   __syncthreads();
   if (pk.stop == 3) {
