@@ -36,6 +36,7 @@ struct GemmP {
   const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
   int a_elu;                    // ELU on A (tokenizer encoder convs)
   int dbg;                      // measurement hook of the decode GEMV (QT_GEMV_DBG): 1 = no A loads, 2 = no MFMA
+  int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))
 };
 
 // SnakeBeta exactly as qt_snake computes it (fp32 math on the stored activation)
@@ -198,29 +199,46 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
 // by select, so every chunk issues its U weight fragments (1 KiB contiguous per wave-instruction), A
 // fragments and gamma before a single wait -- the block keeps all of its weight bytes in flight.
 // Split-K partials reduce through LDS; the epilogue is shared with gemm_wt.
-template <typename WT, typename AT, typename OT, int WPB, int U, bool NORM, bool NTL, bool HALF>
+// Fold F (bf16 weights, rows per block <= 16 / F): the MFMA rows past the block's rows are zero, so the lanes
+// feeding them fetch the block's rows of the next F - 1 k tiles instead of re-fetching a clamped row, and DPP row
+// rotations (row_ror 16/F * t) hand those fragments to the live lanes for the t-th MFMA: 1/F of the activation
+// requests, the same MFMA operands.  Row groups (gridDim.z): block z owns rows [z * p.mr, z * p.mr + p.mr) -- a
+// few-column-tile GEMV gets more blocks without a cross-block split-K reduction (its weight tiles are re-read
+// from L2 by the z blocks; blockIdx.x-major launch keeps a tile's row blocks ntiles apart, same XCD when
+// ntiles % 8 == 0).
+// DPP row_ror:S on each dword of a 16-byte fragment (rotate right: lane l of a 16-lane row receives lane
+// (l - S) mod 16)
+template <int S>
+QT_DEV u32x4_t ror4(u32x4_t x) {
+  u32x4_t r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x[e], 0x120 + S, 0xF, 0xF, false);
+  return r;
+}
+
+template <typename WT, typename AT, typename OT, int WPB, int U, bool NORM, bool NTL, int F>
 __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   constexpr bool BF = sizeof(WT) == 2;
   constexpr int E = BF ? 8 : 4;
   constexpr int KT = 4 * E;
-  static_assert(!HALF || (BF && U % 2 == 0), "HALF: bf16 weights, even U");
+  constexpr int RPF = 16 / F;  // MFMA rows fed by real rows
+  static_assert(F == 1 || (BF && U % F == 0), "fold: bf16 weights, U multiple of F");
   __shared__ float red[WPB][64][4];
   __shared__ float red_ss[WPB][16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lm = lane & 15, lk = lane >> 4;
   const int nt = blockIdx.x, sp = blockIdx.y;
+  const int m0 = blockIdx.z * p.mr;           // first row of this row group
+  const int mr = min(p.mr, p.M - m0);         // rows of this block
   const int ktiles = p.Kp / KT;
   const int kps = (ktiles + p.ks - 1) / p.ks;  // k tiles of this split
   const int ks0 = sp * kps, ks1 = min(ktiles, ks0 + kps);
   const int per = (kps + WPB - 1) / WPB;
   const int kt0 = ks0 + w * per, kt1 = min(ks1, kt0 + per);
-  // HALF (M <= 8): lanes of MFMA rows 8..15 (zero rows) fetch rows 0..7 of the pair's second k tile instead of
-  // re-fetching a clamped row, and a DPP row rotation hands those values to lanes 0..7 for the second MFMA:
-  // half the activation requests, the same MFMA operands
-  const int arow_i = HALF ? (lm & 7) : lm;
-  const int hsel = HALF ? (lm >> 3) : 0;
-  const bool rowok = arow_i < p.M;
-  const int mrow = rowok ? arow_i : p.M - 1;
+  const int arow_i = lm % RPF;  // the block row this lane fetches
+  const int hsel = lm / RPF;    // which k tile of the fold group it fetches
+  const bool rowok = arow_i < mr;
+  const int mrow = m0 + (rowok ? arow_i : mr - 1);
   const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[mrow] : (long long)mrow) * p.lda + lk * E;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   float ssv[E];
@@ -236,11 +254,11 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     if (p.epi == QT_EPI_ADD && nval) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (lk * 4 + i < p.M) pre_out[i] = to_f(((const OT*)p.out)[(long long)(lk * 4 + i) * p.ldo + n]);
+        if (lk * 4 + i < mr) pre_out[i] = to_f(((const OT*)p.out)[(long long)(m0 + lk * 4 + i) * p.ldo + n]);
     }
   }
   const WT* wp = (const WT*)p.W + ((size_t)nt * ktiles) * 64 * E + lane * E;
-  constexpr int NA = HALF ? U / 2 : U;  // A fragments per chunk
+  constexpr int NA = U / F;  // A fragments per chunk
   for (int c = kt0; c < kt1; c += U) {
     u32x4_t wv[U];
     float a[NA][E];
@@ -254,9 +272,9 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     }
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
-      // every lane loads (without HALF, rows >= M re-fetch row M-1 from L2: predicating the load on the row was
+      // every lane loads (with F == 1, rows >= M re-fetch row M-1 from L2: predicating the load on the row was
       // measured slower, profiles/r01_gemv_variants_ab.jsonl)
-      const int kc = min(c + (HALF ? 2 * q + hsel : q), kt1 - 1);
+      const int kc = min(c + F * q + hsel, kt1 - 1);
       if (p.dbg & 1) {
 #pragma unroll
         for (int i = 0; i < E; ++i) a[q][i] = 1.f;
@@ -264,7 +282,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     }
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
-      const bool ok = rowok && (c + (HALF ? 2 * q + hsel : q) < kt1);
+      const bool ok = rowok && (c + F * q + hsel < kt1);
 #pragma unroll
       for (int i = 0; i < E; ++i) {
         float x = ok ? a[q][i] : 0.f;
@@ -273,18 +291,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
       }
       if (p.dbg & 2) {
         acc[0] += __uint_as_float(wv[q][0] ^ wv[q][1] ^ wv[q][2] ^ wv[q][3]) + a[q][0];
-      } else if constexpr (HALF) {
+      } else if constexpr (F > 1) {
         const u32x4_t own = {pack2bf(a[q][0], a[q][1]), pack2bf(a[q][2], a[q][3]), pack2bf(a[q][4], a[q][5]),
                              pack2bf(a[q][6], a[q][7])};
-        u32x4_t par;  // row_ror:8 -- lane l (l % 16 < 8) receives lane l + 8's fragment: the pair's second k tile
-#pragma unroll
-        for (int e = 0; e < 4; ++e) par[e] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)own[e], 0x128, 0xF, 0xF, false);
         const u32x4_t zero = {0u, 0u, 0u, 0u};
-        const u32x4_t a0 = hsel ? zero : own, a1 = hsel ? zero : par;
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a0),
-                                                      __builtin_bit_cast(bf16x8_t, wv[2 * q]), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a1),
-                                                      __builtin_bit_cast(bf16x8_t, wv[2 * q + 1]), acc, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < F; ++t) {
+          // row_ror:(16 - RPF*t) -- lane r receives lane r + RPF*t: the fold group's t-th k tile
+          u32x4_t av = own;
+          if constexpr (F >= 2) if (t == 1) av = ror4<16 - RPF>(own);
+          if constexpr (F >= 4) if (t == 2) av = ror4<16 - 2 * RPF>(own);
+          if constexpr (F >= 4) if (t == 3) av = ror4<16 - 3 * RPF>(own);
+          av = hsel ? zero : av;
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
+                                                        __builtin_bit_cast(bf16x8_t, wv[F * q + t]), acc, 0, 0, 0);
+        }
       } else if constexpr (BF) {
         u32x4_t av = {pack2bf(a[q][0], a[q][1]), pack2bf(a[q][2], a[q][3]), pack2bf(a[q][4], a[q][5]),
                       pack2bf(a[q][6], a[q][7])};
@@ -302,10 +323,12 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < E; ++i) ss += ssv[i];
-    if constexpr (HALF) ss += dpp_f<0x128>(ss);  // + the lane holding the same row's other k tiles
+    // + the lanes holding the same row's other k tiles of the fold group
+    if constexpr (F == 4) ss += dpp_f<0x124>(ss);
+    if constexpr (F >= 2) ss += dpp_f<0x128>(ss);
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
-    if (lk == 0) red_ss[w][lm] = (HALF && lm >= 8) ? 0.f : ss;
+    if (lk == 0) red_ss[w][lm] = lm >= RPF ? 0.f : ss;
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
@@ -378,168 +401,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     for (int i = 0; i < 4; ++i) {
       float up = __shfl_xor(v[i], 8, 64);
       const int m = lk * 4 + i;
-      if (lm < 8 && m < p.M && nt * 8 + lm < (p.N >> 1))
-        out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[i]) * up);
+      if (lm < 8 && m < mr && nt * 8 + lm < (p.N >> 1))
+        out[(long long)(m0 + m) * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[i]) * up);
     }
     return;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = lk * 4 + i;
-    if (m >= p.M || !nval) continue;
-    OT* o = out + (long long)m * p.ldo + n;
+    if (m >= mr || !nval) continue;
+    OT* o = out + (long long)(m0 + m) * p.ldo + n;
     if (p.epi == QT_EPI_ADD) *o = from_f<OT>(pre_out[i] + v[i]);
     else *o = from_f<OT>(v[i]);
   }
-}
-
-// Decode GEMV with the activations staged once per block (bf16 weights, M <= 16, K*M*2 <= 96 KiB).
-// gemv_wt has every wave fetch its own A fragments from L2 next to its weight fragments, so each 1 KiB weight
-// instruction comes with 2 KiB (fp32 A, rows clamped to 16) of L2 traffic through the same TA path.  Here the
-// block first loads A once (fp32 or bf16 rows -> the bf16 MFMA operand, RMSNorm row sums from the fp32 values)
-// into LDS, then CT column tiles x WPT waves (K split WPT ways) stream weights with 2 x U fragments in flight
-// per wave (double-buffered rounds) and read A fragments from LDS.  Partials reduce through LDS; the epilogue
-// matches gemv_wt (bias, activation, colscale, SwiGLU pairing, residual add).
-constexpr int GL_U = 8;
-template <typename AT, typename OT, bool NORM, bool NTL>
-__global__ __launch_bounds__(1024) void gemv_lds(GemmP p, int CT, int WPT) {
-  extern __shared__ unsigned char gl_smem[];
-  const int M = p.M, Kp = p.Kp, ktiles = Kp / 32;
-  const int ALD = Kp + 8;                                   // bf16 row stride (16 B pad)
-  bf16_t* As = (bf16_t*)gl_smem;                            // [M][ALD]
-  float* red = (float*)(gl_smem + (size_t)M * ALD * 2);     // [CT*WPT][64][4]
-  float* ssr = red + (size_t)CT * WPT * 256;                // [16]
-  const int nw = CT * WPT;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int lm = lane & 15, lk = lane >> 4;
-  const int tl = w / WPT, ks = w % WPT;                     // column tile within the block, K part
-  const int ntiles = (p.N + 15) / 16;
-  const int nt = min(blockIdx.x * CT + tl, ntiles - 1);
-  const bool live = blockIdx.x * CT + tl < ntiles;
-  const int per = (ktiles + WPT - 1) / WPT;
-  const int kt0 = ks * per, kt1 = min(ktiles, kt0 + per);
-  // 1. A rows: wave w stages rows w, w + nw, ... (8 elements per lane per step), row sums of squares in fp32
-  for (int m = w; m < M; m += nw) {
-    const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[m] : (long long)m) * p.lda;
-    float ss = 0.f;
-    for (int c = lane * 8; c < Kp; c += 64 * 8) {
-      float v[8];
-      if (c < p.Klog) load8f(arow + c, v);
-      else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = 0.f;
-      }
-      if (NORM) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ss += v[i] * v[i];
-      }
-      *(u32x4_t*)(As + (size_t)m * ALD + c) = u32x4_t{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
-                                                      pack2bf(v[6], v[7])};
-    }
-    if (NORM) {
-      ss = wave_sum_dpp(ss);
-      if (lane == 0) ssr[m] = ss;
-    }
-  }
-  // 2. weight stream: rounds of U fragments, the next round in flight while the current one is multiplied
-  const bf16_t* wp = (const bf16_t*)p.W + ((size_t)nt * ktiles) * 512 + lane * 8;
-  auto load_round = [&](u32x4_t* wv, int c) {
-#pragma unroll
-    for (int u = 0; u < GL_U; ++u) {
-      const int kc = min(c + u, kt1 - 1);
-      if constexpr (NTL) wv[u] = __builtin_nontemporal_load((const u32x4_t*)(wp + (size_t)kc * 512));
-      else wv[u] = *(const u32x4_t*)(wp + (size_t)kc * 512);
-    }
-  };
-  u32x4_t wa[GL_U], wb[GL_U];
-  if (kt0 < kt1) load_round(wa, kt0);
-  __syncthreads();
-  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* arow_l = As + (size_t)min(lm, M - 1) * ALD + lk * 8;
-  auto mma_round = [&](const u32x4_t* wv, int c) {
-#pragma unroll
-    for (int u = 0; u < GL_U; ++u) {
-      if (c + u < kt1) {
-        u32x4_t av = *(const u32x4_t*)(arow_l + (size_t)(c + u) * 32);
-        if (lm >= M) av = u32x4_t{0u, 0u, 0u, 0u};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av),
-                                                      __builtin_bit_cast(bf16x8_t, wv[u]), acc, 0, 0, 0);
-      }
-    }
-  };
-  for (int c = kt0; c < kt1; c += 2 * GL_U) {
-    if (c + GL_U < kt1) load_round(wb, c + GL_U);
-    mma_round(wa, c);
-    if (c + GL_U >= kt1) break;
-    if (c + 2 * GL_U < kt1) load_round(wa, c + 2 * GL_U);
-    mma_round(wb, c + GL_U);
-  }
-  // 3. reduce the WPT K parts of each tile, epilogue by the tile's first wave
-  float* rw = red + (size_t)w * 256 + lane * 4;
-  rw[0] = acc[0]; rw[1] = acc[1]; rw[2] = acc[2]; rw[3] = acc[3];
-  __syncthreads();
-  if (ks != 0 || !live) return;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k2 = 0; k2 < WPT; ++k2) {
-    const float* q = red + (size_t)(tl * WPT + k2) * 256 + lane * 4;
-    v[0] += q[0]; v[1] += q[1]; v[2] += q[2]; v[3] += q[3];
-  }
-  const int n = nt * 16 + lm;
-  const bool nval = n < p.N;
-  const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
-  const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = lk * 4 + i;
-    float x = v[i];
-    if (NORM) x *= rsqrtf((m < M ? ssr[m] : 0.f) / (float)p.Klog + p.eps);
-    x += bias;
-    x = act_f(x, p.act);
-    v[i] = x * cs;
-  }
-  OT* out = (OT*)p.out;
-  if (p.epi == QT_EPI_SWIGLU) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float up = __shfl_xor(v[i], 8, 64);
-      const int m = lk * 4 + i;
-      if (lm < 8 && m < M && nt * 8 + lm < (p.N >> 1))
-        out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[i]) * up);
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = lk * 4 + i;
-    if (m >= M || !nval) continue;
-    OT* o = out + (long long)m * p.ldo + n;
-    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[i]);
-    else *o = from_f<OT>(v[i]);
-  }
-}
-
-template <typename AT, typename OT>
-bool launch_gemv_lds(const GemmP& p, hipStream_t s) {
-  const int ntiles = (p.N + 15) / 16, ktiles = p.Kp / 32;
-  const size_t a_bytes = (size_t)p.M * (p.Kp + 8) * 2;
-  if (a_bytes > 96 * 1024) return false;
-  // column tiles per block: enough blocks for every CU; K split so each wave streams >= 8 k tiles
-  int CT = std::max(1, std::min(4, ntiles / 256));
-  int WPT = 1;
-  while (WPT * 2 * CT <= 16 && ktiles / (WPT * 2) >= 8) WPT *= 2;
-  static const int cfg = [] { const char* e = getenv("QT_GEMV_LDS_CFG"); return e ? atoi(e) : 0; }();  // CT*100+WPT
-  if (cfg) { CT = cfg / 100; WPT = cfg % 100; }
-  const int nw = CT * WPT;
-  const size_t smem = a_bytes + (size_t)nw * 256 * 4 + 16 * 4;
-  const dim3 grid((ntiles + CT - 1) / CT), block(nw * 64);
-  if (p.rms) {
-    if (p.ntl) hipLaunchKernelGGL((gemv_lds<AT, OT, true, true>), grid, block, smem, s, p, CT, WPT);
-    else hipLaunchKernelGGL((gemv_lds<AT, OT, true, false>), grid, block, smem, s, p, CT, WPT);
-  } else {
-    if (p.ntl) hipLaunchKernelGGL((gemv_lds<AT, OT, false, true>), grid, block, smem, s, p, CT, WPT);
-    else hipLaunchKernelGGL((gemv_lds<AT, OT, false, false>), grid, block, smem, s, p, CT, WPT);
-  }
-  return true;
 }
 
 // LDS-tiled implicit GEMM for large M with bf16 weights (codec convs / transposed convs as taps, prefill
@@ -766,26 +640,27 @@ __global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
   }
 }
 
-template <typename WT, typename AT, typename OT, int WPB, int U, bool HALF>
-void launch_gemv_h(const GemmP& p, int nt, hipStream_t s) {
-  const dim3 grid(nt, p.ks), block(WPB * 64);
+template <typename WT, typename AT, typename OT, int WPB, int U, int F>
+void launch_gemv_f(const GemmP& p, int nt, hipStream_t s) {
+  const dim3 grid(nt, p.ks, (p.M + p.mr - 1) / p.mr), block(WPB * 64);
   if (p.ntl) {
-    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, true, HALF>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, true, HALF>), grid, block, 0, s, p);
+    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, true, F>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, true, F>), grid, block, 0, s, p);
   } else {
-    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, false, HALF>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, false, HALF>), grid, block, 0, s, p);
+    if (p.rms) hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, true, false, F>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemv_wt<WT, AT, OT, WPB, U, false, false, F>), grid, block, 0, s, p);
   }
 }
 
-// HALF (M <= 8, bf16 weights): paired k tiles share the activation fetch (QT_GEMV_HALF=0 disables, measurement)
+// fold factor from the rows per block (bf16 weights): 4 for <= 4 rows, 2 for <= 8 (QT_GEMV_FOLD=1 disables)
 template <typename WT, typename AT, typename OT, int WPB, int U>
 void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
-  static const int half_env = [] { const char* e = getenv("QT_GEMV_HALF"); return e ? atoi(e) : 1; }();
+  static const int fold_env = [] { const char* e = getenv("QT_GEMV_FOLD"); return e ? atoi(e) : 4; }();
   if constexpr (sizeof(WT) == 2) {
-    if (half_env && p.M <= 8) return launch_gemv_h<WT, AT, OT, WPB, U, true>(p, nt, s);
+    if (fold_env >= 4 && p.mr <= 4) return launch_gemv_f<WT, AT, OT, WPB, U, 4>(p, nt, s);
+    if (fold_env >= 2 && p.mr <= 8) return launch_gemv_f<WT, AT, OT, WPB, U, 2>(p, nt, s);
   }
-  launch_gemv_h<WT, AT, OT, WPB, U, false>(p, nt, s);
+  launch_gemv_f<WT, AT, OT, WPB, U, 1>(p, nt, s);
 }
 
 // U = k tiles in flight per wave: 8 when a wave owns 5..8 (one round trip instead of two).  Forcing U = 8 on
@@ -803,12 +678,6 @@ template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
-  static const int use_lds = [] { const char* e = getenv("QT_GEMV_LDS"); return e ? atoi(e) : 0; }();
-  if constexpr (sizeof(WT) == 2) {
-    if (use_lds && p.M <= 16 && p.taps == 0 && p.Klog % 8 == 0 && p.gamma == nullptr && !p.a_elu && p.ks == 1 &&
-        launch_gemv_lds<AT, OT>(p, s))
-      return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
-  }
   if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr && !p.a_elu) {
     const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
     if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
@@ -911,10 +780,8 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   const int ntc = (a->N + 15) / 16;
   p.wpb_max = wpb_env > 0 ? wpb_env : (ntc > 512 ? 4 : (ntc > 256 ? 8 : 16));
   const int ntl = (a->N + 15) / 16, ktl = p.Kp / KT;
-  static const int lds_env = [] { const char* e = getenv("QT_GEMV_LDS"); return e ? atoi(e) : 0; }();
-  const bool lds_auto = lds_env && a->w_dtype == QT_BF16 && a->splitk == 0;  // gemv_lds replaces auto split-K
   if (a->M <= 16 && a->taps == 0 && a->K % KT == 0 && a->gamma == nullptr && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN &&
-      a->splitk != 1 && ntl <= 4096 && !lds_auto) {
+      a->splitk != 1 && ntl <= 4096) {
     // auto: split only deep-K shapes on < 256 column tiles (the arrival / partial round trips pay only when they
     // remove weight round trips).  Measured cold, paired-A GEMV, partial loads of four splits in flight:
     // 2048x6144 11.4 (no split) / 10.9 (2) / 10.3 us (4), 1024x3072 8.5 / 7.6 / 7.1 us; other shapes lose.
@@ -928,6 +795,19 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
       p.ks = ks;
       p.cnt = (unsigned*)a->ws;
       p.part = (float*)((char*)a->ws + 4096 * sizeof(unsigned));
+    }
+  }
+  // decode GEMV row groups (bf16 weights): rows split over gridDim.z blocks instead of K over gridDim.y for
+  // shapes with <= 128 column tiles (measured cold, M = 8, two groups of 4 rows with fold 4: talker o 6.0 -> 5.3,
+  // talker down 10.9 (split-K 2) -> 9.4, CP down 7.6 -> 6.5, CP lm_head 4.9 -> 4.5 us; wider shapes lose:
+  // talker qkv 6.7 -> 9.6).  QT_GEMV_RG = n forces n groups, 1 = off, 0 = auto.
+  p.mr = std::max(1, a->M);
+  static const int rg_env = [] { const char* e = getenv("QT_GEMV_RG"); return e ? atoi(e) : 0; }();
+  if (a->M <= 16 && a->taps == 0 && a->w_dtype == QT_BF16 && a->K % KT == 0 && a->gamma == nullptr) {
+    const int rg = rg_env > 0 ? rg_env : ((a->M > 4 && ntl <= 128) ? 2 : 1);
+    if (rg > 1) {
+      p.mr = (a->M + rg - 1) / rg;
+      p.ks = 1;
     }
   }
   hipStream_t s = (hipStream_t)stream;
