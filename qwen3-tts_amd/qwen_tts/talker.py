@@ -125,6 +125,37 @@ def _attn_oproj_ok(st: _Stack) -> bool:
             and ks // kt <= 16)
 
 
+class CPLane:
+    """Rows [b0, b1) of a session's code predictor: one independent chain of the 15 sequential CP steps.  A
+    session's lanes run on concurrent streams inside the captured frame graph (fork after the talker's token choice,
+    join before the next talker step): the CP is latency-bound, so two half-batch chains overlap their kernel
+    latencies, and each kernel sees M = B / lanes rows (the decode GEMV folds its activation fetch accordingly)."""
+
+    def __init__(self, s: "Session", eng: "TalkerEngine", b0: int, b1: int, ws):
+        c, dev = eng.cp, eng.dev
+        self.b0, self.b1, self.nb = b0, b1, b1 - b0
+        nb = self.nb
+        i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
+        # prefill rows (2r, 2r + 1) = (past_hidden, cb0 embedding); decode rows 0..nb-1 of the same slice
+        self.x = s.cp_x[2 * b0:2 * b1]
+        self.kv = ([k[b0:b1] for k in s.cp_kv[0]], [v[b0:b1] for v in s.cp_kv[1]])
+        self.sc = _scratch(2 * nb, c, dev, attn_oproj=True)
+        self.ws = ws
+        self.logits = torch.zeros(nb, eng.Vc, dtype=torch.float32, device=dev)
+        self.tok = s.cp_tok[b0:b1]
+        self.codes = s.codes[b0:b1]
+        rb2 = torch.arange(2 * nb, device=dev, dtype=torch.int32) // 2
+        p2 = torch.arange(2 * nb, device=dev, dtype=torch.int32) % 2
+        self.meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * nb),
+                      "row_batch": rb2, "small_T": 2}
+        rb = torch.arange(nb, dtype=torch.int32, device=dev)
+        self.meta = []
+        for g in range(1, s.G - 1):
+            pos = torch.full((nb,), g + 1, dtype=torch.int32, device=dev)
+            self.meta.append({"rope_pos": pos, "kv_pos": pos.clone(), "row_len": pos + 1, "row_start": i32(nb),
+                              "row_batch": rb, "const_pos": g + 1})
+
+
 @dataclass
 class GenParams:
     max_new_tokens: int = 4096
@@ -168,24 +199,12 @@ class Session:
         self.meta = {"rope_pos": self.ctr[2:2 + B], "kv_pos": self.ctr[2 + B:2 + 2 * B],
                      "row_len": self.ctr[2 + 2 * B:2 + 3 * B], "row_start": i32(B),
                      "row_batch": torch.arange(B, dtype=torch.int32, device=dev)}
-        # code predictor row metadata: prefill (2B rows) and per-step (B rows), static across frames
-        rb2 = torch.arange(2 * B, device=dev, dtype=torch.int32) // 2
-        p2 = torch.arange(2 * B, device=dev, dtype=torch.int32) % 2
-        self.cp_meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * B),
-                         "row_batch": rb2, "small_T": 2}
-        self.cp_meta = []
-        for g in range(1, self.G - 1):
-            pos = torch.full((B,), g + 1, dtype=torch.int32, device=dev)
-            self.cp_meta.append({"rope_pos": pos, "kv_pos": pos.clone(), "row_len": pos + 1, "row_start": i32(B),
-                                 "row_batch": self.meta["row_batch"], "const_pos": g + 1})
         f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.x = f32(B, t.H)
         self.past_hidden = f32(B, t.H)
         self.logits = f32(B, eng.V)
         self.cp_x = f32(2 * B, c.H)
-        self.cp_logits = f32(B, eng.Vc)
         self.sc_t = _scratch(B, t, dev)
-        self.sc_c = _scratch(2 * B, c, dev, attn_oproj=True)
         self.codes = i32(B, max_frames + 2, self.G)
         self.hiddens = f32(B, max_frames + 1, t.H)
         self.tok0 = i32(B)
@@ -197,6 +216,10 @@ class Session:
         self.ws = K.new_workspace(dev)  # split-K scratch private to this session's stream
         self.row_base = 0
         self.graph = None
+        nl = max(1, min(eng.cp_lanes, B))
+        cuts = [B * i // nl for i in range(nl + 1)]
+        self.cp_lanes = [CPLane(self, eng, cuts[i], cuts[i + 1], self.ws if i == 0 else K.new_workspace(dev))
+                         for i in range(nl)]
 
 
 class TalkerEngine:
@@ -236,6 +259,9 @@ class TalkerEngine:
         # decode row groups: the batch is split into this many independent groups, each with its own session,
         # HIP stream and captured frame graph; their latency-bound frames overlap on the GPU
         self.row_groups = int(os.environ.get("QT_ROW_GROUPS", "1"))
+        # code-predictor lanes per session (CPLane): concurrent CP chains inside one frame graph
+        self.cp_lanes = int(os.environ.get("QT_CP_LANES", "1"))
+        self._cp_streams: List[torch.cuda.Stream] = []
         torch.cuda.synchronize()
 
     def _proj_table(self, emb, Hc):
@@ -309,21 +335,24 @@ class TalkerEngine:
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
-        B, t, c, gp = s.B, self.talker, self.cp, s.gp
-        Hc = c.H
+        B, t = s.B, self.talker
         codes_ld = s.codes.shape[1] * self.G
-        # --- code predictor prefill: rows (2b, 2b+1) = (past_hidden[b], codec_embedding(tok0[b])); the odd rows
-        # were written by the talker sampler that chose tok0 (projected embedding table)
-        if self.s2m is not None:
-            K.gemm(s.past_hidden, self.s2m, s.cp_x, B, t.H, 2 * Hc)
-        else:
-            s.cp_x.view(B, 2, Hc)[:, 0].copy_(s.past_hidden)
-        c.forward(s.cp_x, 2 * B, s.cp_meta0, s.cp_kv, s.sc_c, s.cp_L, s.cp_L)
-        self._cp_head(s, s.cp_x.view(-1)[Hc:], 2 * Hc, 0)
-        for g in range(1, self.G - 1):
-            x = s.cp_x[:B]  # written by the previous step's sampler (embedding of the token it chose)
-            c.forward(x, B, s.cp_meta[g - 1], s.cp_kv, s.sc_c, s.cp_L, s.cp_L, decode=True)
-            self._cp_head(s, x, Hc, g)
+        lanes = s.cp_lanes
+        if len(lanes) == 1:
+            self._cp_lane(s, lanes[0])
+        else:  # fork: lanes 1.. on their own streams, lane 0 on the frame's stream; join before the talker step
+            main = torch.cuda.current_stream(self.dev)
+            while len(self._cp_streams) < len(lanes) - 1:
+                self._cp_streams.append(torch.cuda.Stream(device=self.dev))
+            for i in range(1, len(lanes)):
+                st = self._cp_streams[i - 1]
+                st.wait_stream(main)
+                with torch.cuda.stream(st), K.use_workspace(lanes[i].ws):
+                    self._cp_lane(s, lanes[i])
+            with K.use_workspace(lanes[0].ws):
+                self._cp_lane(s, lanes[0])
+            for i in range(1, len(lanes)):
+                main.wait_stream(self._cp_streams[i - 1])
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B)
@@ -334,14 +363,31 @@ class TalkerEngine:
         self._sample_talker(s, s.logits, 1, 0)
         K.advance(s.ctr, 2 + 3 * B)
 
-    def _cp_head(self, s: Session, h, ldh, g):
+    def _cp_lane(self, s: Session, ln: CPLane):
+        """Code predictor for rows [b0, b1): 2-token prefill + 14 decode steps (M:1671-1680)."""
+        t, c = self.talker, self.cp
+        Hc, nb = c.H, ln.nb
+        # --- prefill: rows (2r, 2r+1) = (past_hidden[r], codec_embedding(tok0[r])); the odd rows were written by
+        # the talker sampler that chose tok0 (projected embedding table)
+        if self.s2m is not None:
+            K.gemm(s.past_hidden[ln.b0:ln.b1], self.s2m, ln.x, nb, t.H, 2 * Hc)
+        else:
+            ln.x.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
+        c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L)
+        self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0)
+        for g in range(1, self.G - 1):
+            x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
+            c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True)
+            self._cp_head(s, ln, x, Hc, g)
+
+    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g):
         c, gp = self.cp, s.gp
-        K.gemm(h, self.lm_heads[g], s.cp_logits, s.B, ldh, self.Vc, rms=True, eps=c.eps)
-        K.sample(s.cp_logits, s.B, self.Vc, self.Vc, s.cp_tok, do_sample=gp.subtalker_dosample,
+        K.gemm(h, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
+        K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
-                 seed=gp.seed, step=s.step, substep=1 + g, codes=s.codes, codes_ld=s.codes.shape[1] * self.G,
-                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base,
-                 emb=(self.cp_in_tabs[g], s.cp_x, c.H) if g < self.G - 2 else None)
+                 seed=gp.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
+                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base + ln.b0,
+                 emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
@@ -426,7 +472,7 @@ class TalkerEngine:
         for st in streams:
             main.wait_stream(st)
         for s in sessions:
-            for sc in (s.sc_t, s.sc_c):
+            for sc in [s.sc_t] + [ln.sc for ln in s.cp_lanes]:
                 if "mlp_err" in sc and int(sc["mlp_err"].item()):
                     raise RuntimeError("qt_mlp_decode: in-kernel arrival wait timed out (results invalid)")
         yield sessions, frames, True

@@ -662,6 +662,32 @@ def test_row_groups_identical_to_whole_batch(tiny_models, dtype):
             np.testing.assert_array_equal(a.numpy(), b.numpy())
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cp_lanes_identical_to_one_chain(tiny_models, dtype):
+    """The code predictor as 2 or 3 concurrent lanes (CPLane: forked streams inside the frame graph, graph and
+    eager) reproduces the single-chain codes exactly, sampling included."""
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype=dtype)
+    case = dict(talker_cases()["cv_b3_auto_nospk"], do_sample=True, subtalker_dosample=True, seed=7)
+    ref = None
+    try:
+        for lanes, use_graph in ((1, True), (2, True), (3, True), (2, False)):
+            model.engine.cp_lanes = lanes
+            model.engine._sessions.clear()
+            codes, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg, use_graph=use_graph)
+            if ref is None:
+                ref = codes
+                continue
+            assert len(codes) == len(ref)
+            for a, b in zip(codes, ref):
+                np.testing.assert_array_equal(a.numpy(), b.numpy())
+    finally:
+        model.engine.cp_lanes = 1
+        model.engine._sessions.clear()
+
+
 @pytest.mark.parametrize("ctx,eos,frames", [(1000, False, 30), (1000, True, 24), (2, True, 24), (1000, False, 331)])
 def test_stream_matches_one_shot(tiny_models, ctx, eos, frames):
     """stream(): per utterance the PCM chunks concatenate to exactly the one-shot generate+decode length
