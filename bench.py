@@ -52,7 +52,7 @@ def make_weights(preset, dev, world, rank):
     return cfg, W, CW
 
 
-ROOF_KERNEL = "gemv_wt<bf16,f32,bf16,WPB=4,U=4,rms> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
+ROOF_KERNEL = "gemv_wt<bf16,f32,bf16,WPB=4,U=4,rms,fold=2> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
 
 
 def gateup_bytes(eng, B):
@@ -94,6 +94,48 @@ def kernel_roofline(tts, B, reps=10):
     us = e0.elapsed_time(e1) * 1e3 / n
     byt = gateup_bytes(eng, B)
     return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, launches=n)
+
+
+def attention_roofline(tts, B, L, reps=10):
+    """North-star secondary roofline: the talker decode attention (q/k norm + RoPE + KV append + GQA attention,
+    attn_decode_k) at cache length L, 28 launches over distinct per-layer caches (as in a frame) in a HIP graph.
+    Algorithmic bytes per launch = the K and V rows read: B x Hkv x L x D x 2 x sizeof(bf16)."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    t = eng.talker
+    dev = eng.dev
+    nl = len(t.layers)
+    kc = [torch.randn(B, t.Hkv, L + 1, t.D, device=dev).to(eng.kv_dtype) for _ in range(nl)]
+    vc = [torch.randn(B, t.Hkv, L + 1, t.D, device=dev).to(eng.kv_dtype) for _ in range(nl)]
+    qkv = torch.randn(B, (t.Hq + 2 * t.Hkv) * t.D, device=dev)
+    att = torch.empty(B, t.Hq * t.D, dtype=eng.wdt, device=dev)
+    pos = torch.full((B,), L - 1, dtype=torch.int32, device=dev)
+    rb = torch.arange(B, dtype=torch.int32, device=dev)
+    zero = torch.zeros(B, dtype=torch.int32, device=dev)
+    t.ensure_rope(L + 4, dev)
+    L0 = t.layers[0]
+
+    def run():
+        for i in range(nl):
+            Kn.decode_attention(qkv, B, t.Hq, t.Hkv, t.D, L0.q_norm, L0.k_norm, t.eps, t.cos, t.sin, pos, rb, pos,
+                                zero, kc[i], vc[i], L + 1, att)
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        run()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            run()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            g.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * nl)
+    byt = B * t.Hkv * L * t.D * 2 * kc[0].element_size()
+    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, keys=L)
 
 
 def cpu_baseline(B, prompt, frames, threads):
@@ -198,6 +240,8 @@ def main():
         from qwen_tts.dp import reduce_timing
         dt, audio = reduce_timing(dt, audio, device=dev)
     value = audio / dt
+    # talker cache length at the end of a timed step (prompt + frames), before stream() reuses the sessions
+    L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine._sessions.values())
     # first packet (SURVEY §8 metric): request submit -> first PCM chunk delivered by stream(), p50 of 3 after a
     # warmup, on this rank's batch of B and on a single utterance
     def first_packet(n):
@@ -211,7 +255,7 @@ def main():
     for n in (B, 1):
         first_packet(n)
         fp[n] = 1e3 * float(np.median([first_packet(n) for _ in range(3)]))
-    roof = None
+    roof = attn_roof = None
     if a.roofline and rank == 0:
         r = kernel_roofline(tts, B)
         traffic = None
@@ -222,6 +266,13 @@ def main():
                 "unit": "GB/s", "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),
                 "timed_launches": r["launches"]}
+        # decode attention at the run's mean cache length (prompt + half the frames)
+        L_mean = max(L_end - a.frames // 2, 1)
+        ra = attention_roofline(tts, B, L_mean)
+        attn_roof = {"bound": "hbm", "kernel": f"attn_decode_k (talker decode attention, B={B}, {L_mean} keys)",
+                     "achieved": round(ra["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ra["gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(ra["avg_us"], 2),
+                     "bytes_per_launch": int(ra["bytes"])}
     cpu = None
     if a.cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -238,7 +289,7 @@ def main():
                "rtf_per_utterance": round(per_utt_rtf, 2),
                "first_packet_p50_ms": round(fp[B], 1), "first_packet_p50_ms_b1": round(fp[1], 1),
                "full_batch_latency_p50_ms": round(1e3 * float(np.median(lat)), 1),
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "decode_attention_roofline": attn_roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
