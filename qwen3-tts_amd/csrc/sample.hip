@@ -2,7 +2,8 @@
 // Each thread keeps its V/256 (<= 16) scores in registers (strided, coalesced loads).
 // Greedy: argmax with lowest-index tie break (torch.argmax).
 // Sampling: Temperature -> TopK -> TopP -> softmax -> draw from a Philox-4x32-10 stream keyed by
-// (seed, step, substep, row).  Top-k threshold = exact k-th largest score, found by building its
+// (seed, step, substep, row).  k <= 64 without top-p (the generate() defaults, k = 50): per-wave candidate lists and
+// a Gumbel-max draw in one wave (see sample_k).  Otherwise: top-k threshold = exact k-th largest score, found by building its
 // order-preserving 32-bit key MSB-first (<= 16 block-wide 2-bit steps, no sort); ties at the threshold are kept
 // like TopKLogitsWarper.  The draw is an inverse CDF over a fixed category order (parallel prefix of
 // per-thread masses), so it is an exact sample of the warped distribution; RNG streams differ from
@@ -12,6 +13,7 @@
 
 namespace {
 
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 constexpr int NT = 256;  // threads per row; PER = scores per thread (8 / 12 / 16 for V <= 2048 / 3072 / 4096)
 
 QT_DEV unsigned mulhilo(unsigned a, unsigned b, unsigned* hi) {
@@ -20,9 +22,9 @@ QT_DEV unsigned mulhilo(unsigned a, unsigned b, unsigned* hi) {
   return (unsigned)p;
 }
 
-QT_DEV float philox_uniform(unsigned long long seed, unsigned c0, unsigned c1, unsigned c2) {
+QT_DEV float philox_uniform4(unsigned long long seed, unsigned c0, unsigned c1, unsigned c2, unsigned c3) {
   unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
-  unsigned x0 = c0, x1 = c1, x2 = c2, x3 = 0x9E3779B9u;
+  unsigned x0 = c0, x1 = c1, x2 = c2, x3 = c3;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     unsigned h0, h1;
@@ -34,10 +36,40 @@ QT_DEV float philox_uniform(unsigned long long seed, unsigned c0, unsigned c1, u
   }
   return ((x0 >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
 }
+QT_DEV float philox_uniform(unsigned long long seed, unsigned c0, unsigned c1, unsigned c2) {
+  return philox_uniform4(seed, c0, c1, c2, 0x9E3779B9u);
+}
 
 QT_DEV unsigned okey(float f) {  // order-preserving float -> uint
   unsigned u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+QT_DEV float okey_inv(unsigned k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+
+// One MSB-first 2-bit step of the k-th-largest-key search over N keys per lane, counts summed over the wave:
+// extends the prefix t (count(keys >= t) = cur >= k) by the largest 2-bit digit that keeps >= k keys.
+template <int N>
+QT_DEV void kth_step(const unsigned* key, int k, int bit, unsigned& t, int& cur) {
+  const unsigned c1 = t | (1u << bit), c2 = t | (2u << bit), c3 = t | (3u << bit);
+  int n12 = 0, n3 = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    n12 += (key[j] >= c1 ? 1 : 0) + (key[j] >= c2 ? 0x10000 : 0);
+    n3 += key[j] >= c3 ? 1 : 0;
+  }
+  const int s12 = wave_sum_i(n12), t3 = wave_sum_i(n3);
+  const int t1 = s12 & 0xFFFF, t2 = s12 >> 16;
+  if (t3 >= k) { t = c3; cur = t3; }
+  else if (t2 >= k) { t = c2; cur = t2; }
+  else if (t1 >= k) { t = c1; cur = t1; }
+}
+
+// (best, index) max with lowest-index tie break against the DPP partner CTRL (row-local all-reduce steps)
+template <int CTRL>
+QT_DEV void argmax_dpp(float& best, int& bi) {
+  const float ob = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(best), CTRL, 0xF, 0xF, false));
+  const int oi = __builtin_amdgcn_update_dpp(0, bi, CTRL, 0xF, 0xF, false);
+  if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
 }
 
 QT_DEV float block_sum(float v, float* sh) {
@@ -70,22 +102,43 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   __shared__ int ncand;
   __shared__ unsigned shtk;
   __shared__ float srt[4096];
+  __shared__ __attribute__((aligned(16))) unsigned ck_s[4][64];
+  __shared__ int ci_s[4][64], nc_s[4];
+  __shared__ __attribute__((aligned(16))) int gi_s[16];
+  __shared__ __attribute__((aligned(16))) float gb_s[16];
+  __shared__ unsigned tk_s;
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = p.V;
   const float* lg = p.logits + (long long)r * p.ld;
-  const bool fin = p.finished && p.finished[r];
-  const int ngen = p.n_generated ? *p.n_generated : 1 << 30;
+  // Every global load of the kernel's prologue is issued back to back before the first wait: scores at clamped
+  // indices, the seen flags and the device counters through always-valid pointers (the logits row stands in
+  // when an optional pointer is null), selected afterwards -- a per-element or per-pointer branch made the
+  // compiler wait for each load in turn (one L2 round trip each).
+  const bool pen = p.seen && p.rep_penalty != 1.0f;
+  const unsigned char* sr = pen ? p.seen + (long long)r * V : (const unsigned char*)lg;
+  const int* ngp = p.n_generated ? p.n_generated : (const int*)lg;
+  const int* stpp = p.step ? p.step : (const int*)lg;
+  const unsigned char* fnp = p.finished ? p.finished + r : (const unsigned char*)lg;
   float s[PER];
+  unsigned char sn[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) s[j] = lg[min(tid + j * NT, V - 1)];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) sn[j] = sr[min(tid + j * NT, V - 1)];
+  const int ngr = __hip_atomic_load(ngp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int str = __hip_atomic_load(stpp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int fnr = *fnp;
+  const int ngen = p.n_generated ? ngr : 1 << 30;
+  const unsigned stp = p.step ? (unsigned)str : 0u;
+  const int finv = p.finished ? fnr : 0;
+  const bool eos_mask = p.eos_id >= 0 && (ngen < p.min_new_tokens || p.ignore_eos);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int v = tid + j * NT;
-    float x = -INFINITY;
-    if (v < V) {
-      x = lg[v];
-      if (p.seen && p.rep_penalty != 1.0f && p.seen[(long long)r * V + v]) x = x < 0.f ? x * p.rep_penalty : x / p.rep_penalty;
-      if (p.eos_id >= 0 && v == p.eos_id && (ngen < p.min_new_tokens || p.ignore_eos)) x = -INFINITY;
-      if (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) x = -INFINITY;
-    }
+    float x = s[j];
+    if (pen && sn[j]) x = x < 0.f ? x * p.rep_penalty : x / p.rep_penalty;
+    if ((eos_mask && v == p.eos_id) || (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) || v >= V)
+      x = -INFINITY;
     s[j] = x;
   }
   if (pk.stop == 1) {
@@ -118,16 +171,101 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < PER; ++j) { s[j] *= invT; mx = fmaxf(mx, s[j]); }
-    mx = block_max(mx, sh);
+    unsigned key[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) key[j] = (tid + j * NT < V) ? okey(s[j]) : 0u;  // 0 = no token
+    // Fast top-k (k <= 64, no top-p): the global top-k set lies inside the union of the four waves' own top-k sets.
+    // (1) each wave narrows its keys to <= 64 candidates >= a prefix of its k-th largest key (wave sums only, no
+    // barrier) and compacts them into LDS; (2) wave 0 finds the exact k-th largest key among the <= 256 candidates
+    // (ties kept, TopKLogitsWarper) while every thread draws the Gumbel key of one candidate; (3) the draw is a
+    // Gumbel-max over the kept ones: token = argmax (s_i + G_i), G_i = -log(-log(u_i)), u_i from Philox(seed,
+    // step, substep, row, token) -- an exact sample of softmax(s / T) restricted to the top-k set.  A wave left
+    // with > 64 tied keys falls back to the block search.
+    bool fast = false;
+    if (p.top_k > 0 && p.top_k < V && p.top_k <= 64 && p.top_p >= 1.0f) {
+      int nv = 0;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) nv += key[j] != 0u;
+      int cw = wave_sum_i(nv);
+      unsigned tw = 0u;
+      for (int bit = 30; bit >= 0 && cw > 64; bit -= 2) kth_step<PER>(key, p.top_k, bit, tw, cw);
+      int base = 0;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const bool c = key[j] != 0u && key[j] >= tw;
+        const unsigned long long m = __ballot(c);
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (c && pos < 64) { ck_s[w][pos] = key[j]; ci_s[w][pos] = tid + j * NT; }
+        base += __popcll(m);
+      }
+      if (lane == 0) nc_s[w] = base;
+      if (pk.stop == 6) {
+        if (lane == 0 && base == 12345) p.tok_out[r] = 0;
+        return;
+      }
+      __syncthreads();
+      fast = nc_s[0] <= 64 && nc_s[1] <= 64 && nc_s[2] <= 64 && nc_s[3] <= 64;
+      if (fast) {
+        // wave 0: exact k-th largest key among the <= 256 candidates (4 per lane, 2-bit MSB-first steps with
+        // wave sums, stop at exactly k); meanwhile every thread draws the Gumbel key of candidate (w, lane)
+        if (w == 0) {
+          unsigned ck[4];
+          int tot = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ni = nc_s[i];
+            ck[i] = lane < ni ? ck_s[i][lane] : 0u;
+            tot += ni;
+          }
+          unsigned t = 0u;
+          int cur = tot;
+          for (int bit = 30; bit >= 0 && cur > p.top_k; bit -= 2) kth_step<4>(ck, p.top_k, bit, t, cur);
+          if (lane == 0) tk_s = t;
+        }
+        const bool has = lane < nc_s[w];
+        const unsigned mk = has ? ck_s[w][lane] : 0u;
+        const int mi = has ? ci_s[w][lane] : 0x7fffffff;
+        float g = -INFINITY;
+        if (has && mk > okey(-INFINITY)) {  // masked (-inf) scores are never drawn
+          const float u = philox_uniform4(p.seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)mi);
+          g = okey_inv(mk) - __logf(-__logf(u));
+        }
+        __syncthreads();
+        if (pk.stop == 7) {
+          if (g == 1.5f && tk_s == 12345u) p.tok_out[r] = 0;
+          return;
+        }
+        // Gumbel-max over the kept set (key >= k-th largest: ties kept): DPP argmax in rows, then across rows/waves
+        float best = (has && mk >= tk_s) ? g : -INFINITY;
+        int bi = best > -INFINITY ? mi : 0x7fffffff;
+        argmax_dpp<0xB1>(best, bi);
+        argmax_dpp<0x4E>(best, bi);
+        argmax_dpp<0x141>(best, bi);
+        argmax_dpp<0x140>(best, bi);
+        if ((lane & 15) == 0) { gb_s[w * 4 + (lane >> 4)] = best; gi_s[w * 4 + (lane >> 4)] = bi; }
+        __syncthreads();
+        f32x4_t gb[4];  // all 16 row results in flight at once (8 x 16-byte LDS reads, one wait)
+        i32x4_t gi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { gb[i] = ((const f32x4_t*)gb_s)[i]; gi[i] = ((const i32x4_t*)gi_s)[i]; }
+        best = gb[0][0];
+        bi = gi[0][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i)
+          if (gb[i >> 2][i & 3] > best || (gb[i >> 2][i & 3] == best && gi[i >> 2][i & 3] < bi)) {
+            best = gb[i >> 2][i & 3];
+            bi = gi[i >> 2][i & 3];
+          }
+        tok = bi == 0x7fffffff ? 0 : bi;
+      }
+    }
+    unsigned tk = 0;  // keep keys >= tk
+    if (!fast) mx = block_max(mx, sh);
     if (pk.stop == 2) {
       if (mx == 1234.5f) p.tok_out[r] = 0;
       return;
     }
-    unsigned tk = 0;  // keep keys >= tk
-    if (p.top_k > 0 && p.top_k < V) {
-      unsigned key[PER];
-#pragma unroll
-      for (int j = 0; j < PER; ++j) key[j] = (tid + j * NT < V) ? okey(s[j]) : 0u;
+    if (!fast && p.top_k > 0 && p.top_k < V) {
       // MSB-first construction of the k-th largest key, 2 bits per step.  Counts are per-thread VALU
       // compares summed by packed wave reductions (n1 | n2 << 16, n3) and one barrier per step; the search
       // stops as soon as exactly k keys are >= the prefix (that set is the top-k set).
@@ -188,6 +326,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
       if (tk == 12345u) p.tok_out[r] = 0;
       return;
     }
+    if (!fast) {
     if (p.top_p < 1.0f) {  // rare path: sorted list (descending) for the nucleus cut
       for (int j = 0; j < PER; ++j) {
         const int v = tid + j * NT;
@@ -247,7 +386,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
       if (inc == 1234.5f) p.tok_out[r] = 0;
       return;
     }
-    const float u = philox_uniform(p.seed, (unsigned)(p.step ? *p.step : 0), (unsigned)p.substep, (unsigned)(p.row_base + r)) * total;
+    const float u = philox_uniform(p.seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r)) * total;
     const float excl = inc - mass;
     if (tid == 0) shi[0] = -1;
     __syncthreads();
@@ -269,8 +408,9 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     if (tok < 0) {  // numerical edge: fall back to the argmax of the kept set
       tok = 0;
     }
+    }  // !fast
   }
-  if (fin) tok = p.eos_id;
+  if (finv) tok = p.eos_id;
   if (pk.stop == 5) {
     if (tid == 0) p.tok_out[r] = tok;
     return;
@@ -283,7 +423,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   if (tid != 0) return;
   p.tok_out[r] = tok;
   if (p.codes) {
-    const int st = (p.step ? *p.step : 0) + p.codes_step_off;
+    const int st = (int)stp + p.codes_step_off;
     p.codes[(long long)r * p.codes_ld + (long long)st * p.codes_w + p.codes_col] = tok;
   }
   if (p.seen) p.seen[(long long)r * V + tok] = 1;

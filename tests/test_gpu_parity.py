@@ -517,6 +517,51 @@ def test_sample_topk_support_large_vocab(V, k, ties):
     assert abs((tok2.cpu().long() == top).float().mean().item() - pr[top].item()) < 0.03
 
 
+@pytest.mark.parametrize("V,k", [(2048, 50), (3072, 64), (1024, 1)])
+def test_sample_fast_topk_distribution(V, k):
+    """k <= 64 path (per-wave candidates + Gumbel-max in one wave): every kept token is drawn at its renormalised
+    softmax probability (chi-square-like bound over the whole kept set, same row repeated)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    R = 8192
+    g = torch.Generator().manual_seed(V * 7 + k)
+    row = torch.randn(1, V, generator=g) * 1.5
+    thr = torch.topk(row, k, -1).values[:, -1:]
+    pr = torch.softmax(torch.where(row >= thr, row / 0.9, torch.tensor(-float("inf"))), -1)[0]
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(row.expand(R, V).contiguous().to(dev), R, V, V, tok, do_sample=True, top_k=k, top_p=1.0,
+              temperature=0.9, seed=21, step=torch.full((1,), 3, dtype=torch.int32, device=dev), substep=2)
+    t = tok.cpu().long()
+    assert bool((row[0, t] >= thr[0]).all())
+    freq = torch.bincount(t, minlength=V).float() / R
+    sd = (pr * (1 - pr) / R).sqrt()
+    assert bool(((freq - pr).abs() <= 5 * sd + 1e-3).all())
+
+
+def test_sample_fast_topk_fallbacks():
+    """Shapes the fast path hands back to the block search or must mask: a wave with > 64 tied keys (all scores
+    equal: uniform over the whole row, ties kept), and fewer finite scores than k (-inf never drawn)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    V, R = 2048, 8192
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(torch.zeros(R, V, device=dev), R, V, V, tok, do_sample=True, top_k=50, top_p=1.0, temperature=1.0,
+              seed=2, step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    t = tok.cpu().long()
+    assert t.min() >= 0 and t.max() < V
+    assert len(set(t.tolist())) > V // 2  # ties kept: the draw spreads over the row
+    logits = torch.full((R, V), -float("inf"))
+    fin = torch.tensor([5, 300, 301, 1000, 2047])
+    logits[:, fin] = torch.tensor([0.0, 1.0, -1.0, 0.5, 2.0])
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=50, top_p=1.0, temperature=1.0,
+              seed=3, step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0)
+    t = tok.cpu().long()
+    assert set(t.tolist()) <= set(fin.tolist())
+    pr = torch.softmax(torch.tensor([0.0, 1.0, -1.0, 0.5, 2.0]), -1)
+    freq = torch.tensor([(t == int(f)).float().mean().item() for f in fin])
+    assert (freq - pr).abs().max() < 0.02
+
+
 def test_sample_top_p_support():
     """TopP keeps the smallest top set whose mass reaches top_p (TopPLogitsWarper semantics)."""
     from qwen_tts import kernels as Kn
