@@ -425,12 +425,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
 // registers while the current one is multiplied (double-buffered window, one barrier per chunk).  Weights
 // are the pre-tiled MFMA B fragments (1 KiB per 16 x 32 tile), read through L1/L2 one tap ahead.
 // Row sums of squares (RMSNorm, taps == 1 only) accumulate from the fp32 A values during staging.
+// out-of-line activation for the implicit-GEMM epilogue: inlined, the erf / exp bodies make the epilogue too large
+// to unroll and the accumulators then go through scratch memory
+__attribute__((noinline)) QT_DEV float act_f_call(float x, int act) { return act_f(x, act); }
+
 constexpr int IG_BM = 128, IG_BN = 64, IG_KC = 32, IG_LDSW = 40;  // LDS row stride 40 bf16 (80 B)
 constexpr int IG_GPT = 3;  // staged 8-channel groups per thread (window rows <= 192)
 
-template <typename AT, typename OT, int NT, int MI>
+// G2 = 2 x 2 wave grid: wave (w >> 1, w & 1) owns BM/2 rows x NT/2 column tiles, so each B fragment is fetched by
+// 2 waves instead of 4 (the 4 x 1 layout is L1/TA-bound on the shared B fragments: 4 x NT KiB per k tile per block).
+template <typename AT, typename OT, int NT, int MI, bool G2>
 __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
-  constexpr int BM = 64 * MI;  // output rows per block (MI 16-row tiles per wave)
+  constexpr int BM = 64 * MI;  // output rows per block
+  constexpr int RT = G2 ? BM / 32 : MI;  // 16-row MFMA tiles per wave
+  constexpr int CT = G2 ? NT / 2 : NT;   // 16-column tiles per wave
+  static_assert(!G2 || NT % 2 == 0, "2 x 2 wave grid needs an even column tile count");
   extern __shared__ unsigned char ig_smem[];
   bf16_t* win = (bf16_t*)ig_smem;  // [2][WR][IG_LDSW]
   __shared__ float ss_row[BM];
@@ -443,7 +452,8 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   const int WR = BM + (taps - 1) * dil;
   const int tiles_t = (t_out + BM - 1) / BM;
   const int bi = blockIdx.x / tiles_t, t0 = (blockIdx.x - bi * tiles_t) * BM;
-  const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * NT;
+  const int ntl = (p.N + 15) / 16, nt0 = blockIdx.y * NT + (G2 ? (w & 1) * CT : 0);
+  const int wrow = G2 ? (w >> 1) * (BM / 2) : w * (16 * MI);  // first output row of this wave in the tile
   const int nch = cin_pad / IG_KC, ktiles = p.Kp / IG_KC;
   const AT* A = (const AT*)p.A + (long long)bi * t_in * p.lda;
   const bool norm = p.rms != 0;
@@ -490,15 +500,15 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
     }
   };
 
-  f32x4_t acc[MI][NT];
+  f32x4_t acc[RT][CT];
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < RT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const bf16_t* Wb = (const bf16_t*)p.W + lane * 8;
   auto load_b = [&](u32x4_t* bf, int kt) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
+    for (int j = 0; j < CT; ++j) {
       const int nt = min(nt0 + j, ntl - 1);
       bf[j] = *(const u32x4_t*)(Wb + ((size_t)nt * ktiles + kt) * 512);
     }
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   load_chunk(0);
   store_chunk(0, 0);
   __syncthreads();
-  u32x4_t bcur[NT], bnxt[NT];
+  u32x4_t bcur[CT], bnxt[CT];
   load_b(bcur, 0);  // tap 0 of chunk 0 (k tile = tap * nch + chunk)
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
@@ -517,17 +527,17 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       // one tap ahead: next (tap, chunk) k tile
       const int jn = j + 1 < taps ? j + 1 : 0, cn = j + 1 < taps ? c : c + 1;
       if (cn < nch) load_b(bnxt, jn * nch + cn);
-      u32x4_t af[MI];
+      u32x4_t af[RT];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = *(const u32x4_t*)(wb + (w * (16 * MI) + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
+      for (int i = 0; i < RT; ++i) af[i] = *(const u32x4_t*)(wb + (wrow + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < RT; ++i)
 #pragma unroll
-        for (int q = 0; q < NT; ++q)
+        for (int q = 0; q < CT; ++q)
           acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
                                                               __builtin_bit_cast(bf16x8_t, bcur[q]), acc[i][q], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < NT; ++q) bcur[q] = bnxt[q];
+      for (int q = 0; q < CT; ++q) bcur[q] = bnxt[q];
     }
     if (c + 1 < nch) store_chunk(buf ^ 1, c + 1);
     __syncthreads();
@@ -545,9 +555,9 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   }
   OT* out = (OT*)p.out;
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+  for (int i = 0; i < RT; ++i) {
 #pragma unroll
-    for (int q = 0; q < NT; ++q) {
+    for (int q = 0; q < CT; ++q) {
       const int nt = nt0 + q;
       if (nt >= ntl) continue;
       const int n = nt * 16 + lm;
@@ -557,18 +567,18 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int rl = w * (16 * MI) + i * 16 + lk * 4 + e;
+        const int rl = wrow + i * 16 + lk * 4 + e;
         float x = acc[i][q][e];
         if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
         x += bias;
-        x = act_f(x, p.act);
+        if (p.act != QT_ACT_NONE) x = act_f_call(x, p.act);
         v[e] = x * cs;
       }
       if (p.epi == QT_EPI_SWIGLU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float up = __shfl_xor(v[e], 8, 64);
-          const int t = t0 + w * (16 * MI) + i * 16 + lk * 4 + e;
+          const int t = t0 + wrow + i * 16 + lk * 4 + e;
           if (lm < 8 && t < t_out && nt * 8 + lm < (p.N >> 1))
             out[((long long)bi * t_out + t) * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[e]) * up);
         }
@@ -576,7 +586,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int t = t0 + w * (16 * MI) + i * 16 + lk * 4 + e;
+        const int t = t0 + wrow + i * 16 + lk * 4 + e;
         if (t >= t_out || !nval) continue;
         OT* o = out + ((long long)bi * t_out + t) * p.ldo + n;
         if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[e]);
@@ -699,13 +709,19 @@ int launch(const GemmP& p, hipStream_t s) {
     // column tile per block: 6 x 16 for 96 / 192-channel layers (no idle tiles, the snake-staged window is
     // shared by all of a row tile's columns), else 8 x 16; QT_IGEMM_CFG = "NT,MI" overrides (measurement)
     static const int cfg = [] { const char* e = getenv("QT_IGEMM_CFG"); return e ? atoi(e) * 10 + atoi(e + 2) : 0; }();
+    // QT_IGEMM_G2 = 0 selects the 4 x 1 wave layout (measurement); default 2 x 2
+    static const int g2 = [] { const char* e = getenv("QT_IGEMM_G2"); return e ? atoi(e) : 1; }();
     int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8, mi = 2;
     if (cfg) { ntb = cfg / 10; mi = cfg % 10; }
     const int bm = 64 * mi;
     const int WR = bm + (taps - 1) * dil;
     const size_t smem = (size_t)2 * WR * IG_LDSW * sizeof(bf16_t);
     dim3 grid(batches * ((t_out + bm - 1) / bm), (nt + ntb - 1) / ntb);
-#define IG_GO(N_, M_) hipLaunchKernelGGL((igemm_k<AT, OT, N_, M_>), grid, dim3(256), smem, s, p)
+#define IG_GO(N_, M_)                                                                            \
+  do {                                                                                           \
+    if (g2) hipLaunchKernelGGL((igemm_k<AT, OT, N_, M_, true>), grid, dim3(256), smem, s, p);    \
+    else hipLaunchKernelGGL((igemm_k<AT, OT, N_, M_, false>), grid, dim3(256), smem, s, p);      \
+  } while (0)
     if (ntb == 6 && mi == 2) IG_GO(6, 2);
     else if (ntb == 6 && mi == 1) IG_GO(6, 1);
     else if (ntb == 4 && mi == 2) IG_GO(4, 2);
