@@ -431,6 +431,9 @@ __attribute__((noinline)) QT_DEV float act_f_call(float x, int act) { return act
 
 constexpr int IG_BM = 128, IG_BN = 64, IG_KC = 32, IG_LDSW = 40;  // LDS row stride 40 bf16 (80 B)
 constexpr int IG_GPT = 3;  // staged 8-channel groups per thread (window rows <= 192)
+#ifndef IG_PD
+#define IG_PD 1  // B-fragment prefetch distance in k tiles (2-4 measured slower: codec 41.0 / 34.1 / 38.2 vs 31.0 ms)
+#endif
 
 // G2 = 2 x 2 wave grid: wave (w >> 1, w & 1) owns BM/2 rows x NT/2 column tiles, so each B fragment is fetched by
 // 2 waves instead of 4 (the 4 x 1 layout is L1/TA-bound on the shared B fragments: 4 x NT KiB per k tile per block).
@@ -517,30 +520,43 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   load_chunk(0);
   store_chunk(0, 0);
   __syncthreads();
-  u32x4_t bcur[CT], bnxt[CT];
-  load_b(bcur, 0);  // tap 0 of chunk 0 (k tile = tap * nch + chunk)
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nch) load_chunk(c + 1);
-    const bf16_t* wb = win + (size_t)buf * WR * IG_LDSW;
-    for (int j = 0; j < taps; ++j) {
-      // one tap ahead: next (tap, chunk) k tile
-      const int jn = j + 1 < taps ? j + 1 : 0, cn = j + 1 < taps ? c : c + 1;
-      if (cn < nch) load_b(bnxt, jn * nch + cn);
-      u32x4_t af[RT];
+  // B fragments PD k tiles ahead (a ring of PD register sets, the step loop unrolled by PD so every set index is a
+  // compile-time constant): one tap of MFMA work was too little to cover an L2 round trip.  Steps run over
+  // (chunk c, tap j) in chunk-major order; k tile = j * nch + c.
+  constexpr int PD = IG_PD;
+  const int S = nch * taps;
+  u32x4_t bb[PD][CT];
+  int pc = 0, pj = 0;  // (chunk, tap) of the next k tile to prefetch
 #pragma unroll
-      for (int i = 0; i < RT; ++i) af[i] = *(const u32x4_t*)(wb + (wrow + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
+  for (int u = 0; u < PD; ++u) {
+    if (u < S) load_b(bb[u], pj * nch + pc);
+    if (++pj == taps) { pj = 0; ++pc; }
+  }
+  int c = 0, j = 0;
+  for (int s0 = 0; s0 < S; s0 += PD) {
 #pragma unroll
-      for (int i = 0; i < RT; ++i)
+    for (int u = 0; u < PD; ++u) {
+      if (s0 + u < S) {
+        if (j == 0 && c + 1 < nch) load_chunk(c + 1);
+        const bf16_t* wb = win + (size_t)(c & 1) * WR * IG_LDSW;
+        u32x4_t af[RT];
 #pragma unroll
-        for (int q = 0; q < CT; ++q)
-          acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
-                                                              __builtin_bit_cast(bf16x8_t, bcur[q]), acc[i][q], 0, 0, 0);
+        for (int i = 0; i < RT; ++i) af[i] = *(const u32x4_t*)(wb + (wrow + i * 16 + lm + j * dil) * IG_LDSW + lk * 8);
 #pragma unroll
-      for (int q = 0; q < CT; ++q) bcur[q] = bnxt[q];
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+          for (int q = 0; q < CT; ++q)
+            acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                                __builtin_bit_cast(bf16x8_t, bb[u][q]), acc[i][q], 0, 0, 0);
+        if (pc < nch) load_b(bb[u], pj * nch + pc);
+        if (++pj == taps) { pj = 0; ++pc; }
+        if (j == taps - 1) {
+          if (c + 1 < nch) store_chunk((c & 1) ^ 1, c + 1);
+          __syncthreads();
+        }
+        if (++j == taps) { j = 0; ++c; }
+      }
     }
-    if (c + 1 < nch) store_chunk(buf ^ 1, c + 1);
-    __syncthreads();
   }
   if (norm) {  // rows 0..127 staged by 4 consecutive lanes each (window == tile when taps == 1)
 #pragma unroll
