@@ -635,8 +635,43 @@ __global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
     wsh[k] = to_f(W[(size_t)kt * 64 * E + (kin / E) * 16 * E + (kin % E)]);
   }
   float acc = 0.f;
+  // vector staging (8 channels = one 16-byte load per group, every load of a chunk issued before the first use;
+  // clamped addresses, no branch around the loads) when the channel layout allows it
+  const bool vec = sizeof(AT) == 2 && p.cin % 8 == 0 && p.lda % 8 == 0 && WR * (KC / 8) <= 256 * 8;
   for (int c0 = 0; c0 < p.cin; c0 += KC) {
     __syncthreads();
+    if (vec) {
+      float v[8][8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int g = tid + i * 256, r = min(g >> 2, WR - 1), ch = min(c0 + (g & 3) * 8, p.cin - 8);
+        const int ti = min(max(t0 + p.t_off + r, 0), p.t_in - 1);
+        load8f(A + (long long)ti * p.lda + ch, v[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int g = tid + i * 256, r = g >> 2, cl = (g & 3) * 8, c = c0 + cl;
+        const int ti = t0 + p.t_off + r;
+        if (r >= WR) continue;
+        const bool ok = ti >= 0 && ti < p.t_in && c < p.cin;
+        float sa[8], sb[8];  // SnakeBeta parameters of the group's 8 channels: two vector loads
+        if (p.sn_a) {
+          load8f(p.sn_a + min(c, p.cin - 8), sa);
+          load8f(p.sn_ib + min(c, p.cin - 8), sb);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = 0.f;
+          if (ok) {
+            x = v[i][e];
+            if (p.a_elu) x = elu_f(x);
+            if (p.sn_a) x = snake1(x, sa[e], sb[e]);
+            if (sizeof(WT) == 2) x = __uint_as_float((unsigned)f2bf(x) << 16);  // bf16 operand, as the MFMA paths
+          }
+          c1_win[r * WS + cl + e] = x;
+        }
+      }
+    } else {
     for (int q = tid; q < WR * KC; q += 256) {
       const int r = q / KC, c = c0 + q % KC;
       const int ti = t0 + p.t_off + r;
@@ -648,6 +683,7 @@ __global__ __launch_bounds__(256) void conv_n1_k(GemmP p) {
         if (sizeof(WT) == 2) v = __uint_as_float((unsigned)f2bf(v) << 16);  // bf16 operand, as the MFMA paths
       }
       c1_win[r * WS + q % KC] = v;
+    }
     }
     __syncthreads();
     for (int j = 0; j < taps; ++j) {
