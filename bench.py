@@ -241,7 +241,7 @@ def main():
         dt, audio = reduce_timing(dt, audio, device=dev)
     value = audio / dt
     # talker cache length at the end of a timed step (prompt + frames), before stream() reuses the sessions
-    L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine._sessions.values())
+    L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine.all_sessions())
     # first packet (SURVEY §8 metric): request submit -> first PCM chunk delivered by stream(), p50 of 3 after a
     # warmup, on this rank's batch of B and on a single utterance
     def first_packet(n):

@@ -208,6 +208,10 @@ typedef struct qt_sample_args {
   /* optional next-step input: emb_out[r*emb_ld + i] = emb_table[tok*emb_dim + i], i < emb_dim (fp32) -- the
    * embedding of the chosen token (pre-projected when the model has small_to_mtp), written by the sampler */
   const float* emb_table; int emb_dim; float* emb_out; long long emb_ld;
+  /* optional device seed (read when the sampler runs, so a captured graph draws a fresh Philox stream per
+   * request without recapture); NULL -> `seed` above */
+  const unsigned long long* seed_ptr;
+  float debug_u;  /* < 0: off.  Tests only: replaces the unit uniform of the inverse-CDF draw (1.0 -> u = total) */
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 

@@ -119,6 +119,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   const int* ngp = p.n_generated ? p.n_generated : (const int*)lg;
   const int* stpp = p.step ? p.step : (const int*)lg;
   const unsigned char* fnp = p.finished ? p.finished + r : (const unsigned char*)lg;
+  const unsigned long long* sdp = p.seed_ptr ? p.seed_ptr : (const unsigned long long*)lg;
   float s[PER];
   unsigned char sn[PER];
 #pragma unroll
@@ -128,9 +129,11 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   const int ngr = __hip_atomic_load(ngp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int str = __hip_atomic_load(stpp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int fnr = *fnp;
+  const unsigned long long sdv = __hip_atomic_load(sdp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int ngen = p.n_generated ? ngr : 1 << 30;
   const unsigned stp = p.step ? (unsigned)str : 0u;
   const int finv = p.finished ? fnr : 0;
+  const unsigned long long seed = p.seed_ptr ? sdv : p.seed;
   const bool eos_mask = p.eos_id >= 0 && (ngen < p.min_new_tokens || p.ignore_eos);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
         const int mi = has ? ci_s[w][lane] : 0x7fffffff;
         float g = -INFINITY;
         if (has && mk > okey(-INFINITY)) {  // masked (-inf) scores are never drawn
-          const float u = philox_uniform4(p.seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)mi);
+          const float u = philox_uniform4(seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)mi);
           g = okey_inv(mk) - __logf(-__logf(u));
         }
         __syncthreads();
@@ -368,29 +371,37 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
       e[j] = (tid + j * NT < V && okey(s[j]) >= tk && s[j] > -INFINITY) ? __expf(s[j] - mx) : 0.f;
       mass += e[j];
     }
-    // inclusive prefix of per-thread masses (wave scan + wave offsets)
-    float inc = mass;
+    // inclusive prefix of per-thread masses (wave scan + wave offsets).  Every bound is formed as off + scan, so
+    // thread t's exclusive bound is bit-identical to thread t-1's inclusive one (float + is commutative: across a
+    // wave edge both are sh[0] + ... + sh[w-1] in the same order) and the last thread's inclusive bound is
+    // `total`: the intervals [excl, inc) tile [0, total) with no gaps.
+    float scan = mass;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      float y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
+      float y = __shfl_up(scan, o, 64);
+      if (lane >= o) scan += y;
     }
+    float prev = __shfl_up(scan, 1, 64);
     __syncthreads();
-    if (lane == 63) sh[w] = inc;
+    if (lane == 63) sh[w] = scan;
     __syncthreads();
     float off = 0.f;
     for (int i = 0; i < w; ++i) off += sh[i];
-    const float total = sh[0] + sh[1] + sh[2] + sh[3];
-    inc += off;
+    const float total = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    const float inc = scan + off;
+    const float excl = lane == 0 ? off : prev + off;
     if (pk.stop == 4) {
       if (inc == 1234.5f) p.tok_out[r] = 0;
       return;
     }
-    const float u = philox_uniform(p.seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r)) * total;
-    const float excl = inc - mass;
+    const float uu = p.debug_u >= 0.f ? p.debug_u : philox_uniform(seed, stp, (unsigned)p.substep,
+                                                                   (unsigned)(p.row_base + r));
+    const float u = uu * total;  // may round up to `total` itself
     if (tid == 0) shi[0] = -1;
     __syncthreads();
-    if (mass > 0.f && u >= excl && (u < inc || tid == NT - 1 || inc >= total)) {
+    // the interval holding u claims the draw; u >= total (rounding) goes to the last thread with mass, whose
+    // inclusive bound equals total (the threads after it add exact zeros)
+    if (mass > 0.f && u >= excl && (u < inc || inc >= total)) {
       float cum = excl;
       int pick = -1;
 #pragma unroll
@@ -405,8 +416,27 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     }
     __syncthreads();
     tok = shi[0];
-    if (tok < 0) {  // numerical edge: fall back to the argmax of the kept set
-      tok = 0;
+    if (tok < 0) {  // no positive mass survived (cannot happen with finite scores): argmax of the kept set
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int v = tid + j * NT;
+        if (v < V && okey(s[j]) >= tk && (s[j] > best || (s[j] == best && v < bi))) { best = s[j]; bi = v; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        float ob = __shfl_xor(best, o, 64);
+        int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      __syncthreads();
+      if (lane == 0) { sh[w] = best; shi[w] = bi; }
+      __syncthreads();
+      best = sh[0]; bi = shi[0];
+      for (int i = 1; i < 4; ++i)
+        if (sh[i] > best || (sh[i] == best && shi[i] < bi)) { best = sh[i]; bi = shi[i]; }
+      tok = bi == 0x7fffffff ? 0 : bi;
     }
     }  // !fast
   }

@@ -76,7 +76,8 @@ class SampleArgs(ctypes.Structure):
                 ("temperature", c_float), ("seed", c_ull), ("step", c_void_p), ("substep", c_int),
                 ("tok_out", c_void_p), ("codes", c_void_p), ("codes_ld", c_ll), ("codes_w", c_int),
                 ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int),
-                ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll)]
+                ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll),
+                ("seed_ptr", c_void_p), ("debug_u", c_float)]
 
 
 class MlpArgs(ctypes.Structure):

@@ -161,7 +161,7 @@ class TTSModel:
     def generate(self, input_ids=None, instruct_ids=None, ref_ids=None, voice_clone_prompt=None, languages=None,
                  speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                  temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
-                 subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=0,
+                 subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
                  use_graph=True, **kwargs):
         """Same contract as Qwen3TTSForConditionalGeneration.generate (M:2022-2292):
         returns (list of [F_i,16] int64 codes, list of [F_i,H] last hidden states)."""
@@ -178,7 +178,7 @@ class TTSModel:
     def stream(self, input_ids=None, instruct_ids=None, ref_ids=None, voice_clone_prompt=None, languages=None,
                speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
-               subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=0,
+               subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
                first_chunk_frames=12, chunk_frames=48, left_context=325, use_graph=True, **kwargs):
         """Streaming generation (the reference has none): yields (row, pcm, last) as frames finish.
 

@@ -170,12 +170,21 @@ class GenParams:
     eos_token_id: Optional[int] = None
     repetition_penalty: float = 1.05
     ignore_eos: bool = False
-    seed: int = 0
+    # Philox key of this request's draws.  None (default): a fresh one per generate() call drawn from torch's
+    # default CPU generator, so repeated calls differ like the reference's torch.multinomial draws and
+    # torch.manual_seed makes them reproducible.  It lives in a device word read by the samplers, so it is not
+    # part of the session key: a new seed replays the same captured graph.
+    seed: Optional[int] = None
 
     def key(self):
         return (self.do_sample, self.top_k, self.top_p, self.temperature, self.subtalker_dosample,
                 self.subtalker_top_k, self.subtalker_top_p, self.subtalker_temperature, self.eos_token_id,
-                self.repetition_penalty, self.ignore_eos, self.seed)
+                self.repetition_penalty, self.ignore_eos)
+
+    def resolve_seed(self) -> int:
+        if self.seed is not None:
+            return int(self.seed) & (2 ** 63 - 1)
+        return int(torch.randint(0, 2 ** 63 - 1, (1,)).item())
 
 
 class Session:
@@ -214,8 +223,10 @@ class Session:
         self.trailing = f32(B, max_frames + 1, t.H)
         self.pad_embed = f32(t.H)
         self.ws = K.new_workspace(dev)  # split-K scratch private to this session's stream
+        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox key, read by the captured samplers
         self.row_base = 0
         self.graph = None
+        self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
         nl = max(1, min(eng.cp_lanes, B))
         cuts = [B * i // nl for i in range(nl + 1)]
         self.cp_lanes = [CPLane(self, eng, cuts[i], cuts[i + 1], self.ws if i == 0 else K.new_workspace(dev))
@@ -254,7 +265,7 @@ class TalkerEngine:
         Hc = cc["hidden_size"]
         self.cp_in_tabs = [self._proj_table(self.ecp[g], Hc) for g in range(self.G - 2)]
         self.cp_in_tab0 = self._proj_table(self.emb0, Hc)
-        self._sessions: Dict[tuple, Session] = {}
+        self._sessions: Dict[tuple, List[Session]] = {}
         self._streams: List[torch.cuda.Stream] = []
         # decode row groups: the batch is split into this many independent groups, each with its own session,
         # HIP stream and captured frame graph; their latency-bound frames overlap on the GPU
@@ -302,17 +313,40 @@ class TalkerEngine:
 
     # ---------------------------------------------------------------- sessions / graph
     def session(self, B, P, max_frames, gp: GenParams, row_base: int = 0) -> Session:
+        """A free session of this shape, marked busy (release() hands it back).  A session held by a live request
+        (e.g. a suspended stream() generator) is never shared: a concurrent request of the same shape gets a
+        session of its own (own KV cache, counters and captured graph)."""
         P_cap = max(64, (P + 63) // 64 * 64)
         key = (B, max_frames, gp.key(), row_base)
-        s = self._sessions.get(key)
-        if s is None or s.P_cap < P:
-            if any(k[1:3] != key[1:3] for k in self._sessions) or len(self._sessions) >= 8:
-                self._sessions.clear()  # keep only the live family of sessions (HBM)
-            s = Session(self, B, P_cap, max_frames, gp)
-            s.row_base = row_base
-            self.talker.ensure_rope(s.Lmax + 4, self.dev)
-            self._sessions[key] = s
+        pool = self._sessions.setdefault(key, [])
+        for s in pool:
+            if not s.busy and s.P_cap >= P:
+                s.busy = True
+                return s
+        # HBM: drop idle sessions of other (max_frames, params) families and idle ones too small for P
+        for k in list(self._sessions):
+            if k[1:3] != key[1:3] or k == key:
+                self._sessions[k] = [s for s in self._sessions[k] if s.busy]
+        idle = [s for ss in self._sessions.values() for s in ss if not s.busy]
+        if len(idle) >= 8:
+            for k in list(self._sessions):
+                self._sessions[k] = [s for s in self._sessions[k] if s.busy]
+        for k in [k for k, v in self._sessions.items() if not v and k != key]:
+            del self._sessions[k]
+        s = Session(self, B, P_cap, max_frames, gp)
+        s.row_base = row_base
+        self.talker.ensure_rope(s.Lmax + 4, self.dev)
+        self._sessions.setdefault(key, []).append(s)
+        s.busy = True
         return s
+
+    @staticmethod
+    def release(sessions):
+        for s in sessions:
+            s.busy = False
+
+    def all_sessions(self) -> List[Session]:
+        return [s for ss in self._sessions.values() for s in ss]
 
     def _stream(self, i):
         while len(self._streams) <= i:
@@ -329,7 +363,7 @@ class TalkerEngine:
                  n_generated=s.n_gen, min_new_tokens=2, eos_id=eos,
                  suppress=(self.V - 1024, self.V, self.tc["codec_eos_token_id"]), ignore_eos=gp.ignore_eos,
                  finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
-                 temperature=gp.temperature, seed=gp.seed, step=s.step, substep=substep, codes=s.codes,
+                 temperature=gp.temperature, seed_ptr=s.seed, step=s.step, substep=substep, codes=s.codes,
                  codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off,
                  row_base=s.row_base, emb=(self.cp_in_tab0, s.cp_x.view(-1)[self.cp.H:], 2 * self.cp.H))
 
@@ -385,7 +419,7 @@ class TalkerEngine:
         K.gemm(h, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
-                 seed=gp.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
+                 seed_ptr=s.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
                  codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base + ln.b0,
                  emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None)
 
@@ -400,10 +434,11 @@ class TalkerEngine:
         each row's Philox stream) is the same as decoding the batch whole."""
         it = self.decode_iter(embeds, mask, trailing, tts_pad, gp, use_graph=use_graph, on_frames=on_frames,
                               groups=groups)
-        sessions, frames = None, 0
-        for sessions, frames, _ in it:
-            pass
-        return self.collect(sessions, frames)
+        out = None
+        for sessions, frames, final in it:
+            if final:  # collected while the sessions are still held by this request
+                out = self.collect(sessions, frames)
+        return out
 
     def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
                     groups: Optional[int] = None, every: int = 0, first: int = 0):
@@ -414,20 +449,28 @@ class TalkerEngine:
         B, P, H = embeds.shape
         G = max(1, min(groups or self.row_groups, B))
         max_frames = max(gp.max_new_tokens - 1, 0)
+        seed = gp.resolve_seed()
         cuts = [B * i // G for i in range(G + 1)]
         main = torch.cuda.current_stream(self.dev)
         sessions, streams = [], []
-        for gi in range(G):
-            b0, b1 = cuts[gi], cuts[gi + 1]
-            st = self._stream(gi) if G > 1 else main
-            st.wait_stream(main)
-            s = self.session(b1 - b0, P, max(max_frames, 1), gp, row_base=b0)
-            with torch.cuda.stream(st), K.use_workspace(s.ws):
-                self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad)
-                if max_frames > 0 and use_graph and s.graph is None:
-                    s.graph = self._capture(s)
-            sessions.append(s)
-            streams.append(st)
+        try:
+            for gi in range(G):
+                b0, b1 = cuts[gi], cuts[gi + 1]
+                st = self._stream(gi) if G > 1 else main
+                st.wait_stream(main)
+                s = self.session(b1 - b0, P, max(max_frames, 1), gp, row_base=b0)
+                sessions.append(s)
+                with torch.cuda.stream(st), K.use_workspace(s.ws):
+                    self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad, seed)
+                    if max_frames > 0 and use_graph and s.graph is None:
+                        s.graph = self._capture(s)
+                streams.append(st)
+            yield from self._frames(sessions, streams, max_frames, use_graph, on_frames, every, first)
+        finally:
+            self.release(sessions)
+
+    def _frames(self, sessions, streams, max_frames, use_graph, on_frames, every, first):
+        main = torch.cuda.current_stream(self.dev)
         frames = 0
         check_every = 8
         next_yield = first or every
@@ -492,7 +535,7 @@ class TalkerEngine:
                 out_h.append(hid[b, :L])
         return out_c, out_h
 
-    def _prefill(self, s: Session, embeds, mask, trailing, tts_pad):
+    def _prefill(self, s: Session, embeds, mask, trailing, tts_pad, seed: int):
         """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s."""
         B, P, H = embeds.shape
         t = self.talker
@@ -500,6 +543,7 @@ class TalkerEngine:
         # reset per-request state
         for z in (s.seen, s.finished, s.codes, s.ctr):
             z.zero_()
+        s.seed.fill_(seed)
         # stale K/V beyond each row's valid range is never read (row_start/row_len bound every read)
         Ttr = trailing.shape[1]
         s.pad_embed.copy_(tts_pad.reshape(-1).float())
@@ -536,7 +580,7 @@ class TalkerEngine:
 
     def _capture(self, s: Session):
         # the graph must not see the prefill-time counter values: it only reads device memory
-        snap = s.ctr.clone(), s.seen.clone(), s.finished.clone(), s.codes.clone(), s.tok0.clone()
+        snap = s.ctr.clone(), s.seen.clone(), s.finished.clone(), s.codes.clone(), s.tok0.clone(), s.seed.clone()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
@@ -546,5 +590,5 @@ class TalkerEngine:
         torch.cuda.current_stream().wait_stream(side)
         # capture does not execute kernels on ROCm/CUDA; restore anyway for safety
         s.ctr.copy_(snap[0]); s.seen.copy_(snap[1]); s.finished.copy_(snap[2]); s.codes.copy_(snap[3])
-        s.tok0.copy_(snap[4])
+        s.tok0.copy_(snap[4]); s.seed.copy_(snap[5])
         return g

@@ -43,8 +43,9 @@ class FallbackProcessor:
 def load_processor(path: str):
     """The checkpoint's Qwen2 BPE tokenizer when its files are present (the reference loads it through
     AutoProcessor, W:103-108): `tokenizer_config.json` + `vocab.json` / `merges.txt` (or `tokenizer.json`) via
-    transformers' AutoTokenizer from the local directory; a bare `tokenizer.json` via the `tokenizers` library;
-    otherwise the deterministic stand-in above."""
+    transformers' AutoTokenizer from the local directory; a bare `tokenizer.json` via the `tokenizers` library.
+    The deterministic stand-in above is used only for the packaged synthetic presets: a real checkpoint
+    directory without tokenizer files raises FileNotFoundError instead of silently hashing text."""
     if os.path.exists(os.path.join(path, "tokenizer_config.json")) and (
             os.path.exists(os.path.join(path, "vocab.json")) or os.path.exists(os.path.join(path, "tokenizer.json"))):
         from transformers import AutoTokenizer
@@ -67,4 +68,9 @@ def load_processor(path: str):
                 return {"input_ids": torch.tensor([tok.encode(text).ids], dtype=torch.long)}
 
         return _P()
-    return FallbackProcessor()
+    from .weights import is_preset_dir
+    if is_preset_dir(path):
+        return FallbackProcessor()
+    raise FileNotFoundError(
+        f"no Qwen2 BPE tokenizer in {path!r}: expected tokenizer_config.json + vocab.json/merges.txt, or "
+        "tokenizer.json (the stand-in tokenizer is reserved for the packaged synthetic presets)")

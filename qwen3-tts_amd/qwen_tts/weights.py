@@ -22,7 +22,7 @@ HUB_ALIASES = {
     "qwen/qwen3-tts-12hz-1.7b-voicedesign": "1.7b-voicedesign",
     "qwen/qwen3-tts-12hz-1.7b-base": "1.7b-base",
     "qwen/qwen3-tts-12hz-0.6b-customvoice": "0.6b-customvoice",
-    "qwen/qwen3-tts-12hz-0.6b-base": "1.7b-base",
+    "qwen/qwen3-tts-12hz-0.6b-base": "0.6b-base",
     "qwen/qwen3-tts-tokenizer-12hz": "1.7b-customvoice/speech_tokenizer",
 }
 

@@ -94,3 +94,21 @@ def frontend_cases():
                      spk=[24000, 7777]),
         "full": dict(enc={"single": [72000], "batch": [50000, 72000]}, spk=[72000]),
     }
+
+
+def write_test_tokenizer(path):
+    """A small byte-level BPE tokenizer saved in the Hugging Face layout of a Qwen2 checkpoint
+    (tokenizer_config.json + tokenizer.json, special tokens included): real checkpoint directories must carry
+    tokenizer files (the hash stand-in is reserved for the packaged presets).  Returns the tokenizer."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    from transformers import PreTrainedTokenizerFast
+    tk = Tokenizer(models.BPE())
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=300, special_tokens=["<|im_start|>", "<|im_end|>"],
+                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
+    tk.train_from_iterator(["hello world, this is a voice clone test", "assistant user text"] * 20, tr)
+    hf = PreTrainedTokenizerFast(tokenizer_object=tk)
+    hf.add_special_tokens({"additional_special_tokens": ["<|im_start|>", "<|im_end|>"]})
+    hf.save_pretrained(str(path))
+    return hf

@@ -233,7 +233,7 @@ def make_frontend(preset, kind, fname):
 
 def make_specs():
     specs = {}
-    for p in ("tiny-customvoice", "tiny-base", "1.7b-customvoice", "0.6b-customvoice", "1.7b-base"):
+    for p in ("tiny-customvoice", "tiny-base", "1.7b-customvoice", "0.6b-customvoice", "1.7b-base", "0.6b-base"):
         m, _ = build_ref_model(p, meta=True)
         specs[p] = {k: list(v.shape) for k, v in m.state_dict().items()}
         d, _ = build_ref_codec(p, meta=True)

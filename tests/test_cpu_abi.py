@@ -18,26 +18,48 @@ def test_library_exports_every_declared_symbol():
 def test_qwen2_bpe_files_are_used(tmp_path):
     """A checkpoint directory holding a Qwen2-style BPE tokenizer (tokenizer_config.json + vocab.json /
     merges.txt, as written by save_pretrained) is tokenised by that tokenizer, special tokens included
-    (the reference loads it via AutoProcessor, W:103-108); without the files the stand-in is used."""
+    (the reference loads it via AutoProcessor, W:103-108); without the files only the packaged presets fall back
+    to the stand-in."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "qwen3-tts_amd"))
-    from tokenizers import Tokenizer, models, pre_tokenizers, trainers, decoders
-    from transformers import PreTrainedTokenizerFast
+    from cases import write_test_tokenizer
     from qwen_tts.text import FallbackProcessor, load_processor
-    tk = Tokenizer(models.BPE())
-    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
-    tk.decoder = decoders.ByteLevel()
-    tr = trainers.BpeTrainer(vocab_size=300, special_tokens=["<|im_start|>", "<|im_end|>"],
-                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
-    tk.train_from_iterator(["hello world, this is a voice clone test", "assistant user text"] * 20, tr)
-    hf = PreTrainedTokenizerFast(tokenizer_object=tk)
-    hf.add_special_tokens({"additional_special_tokens": ["<|im_start|>", "<|im_end|>"]})
-    hf.save_pretrained(str(tmp_path))
+    hf = write_test_tokenizer(tmp_path)
     assert os.path.exists(tmp_path / "tokenizer_config.json")
     proc = load_processor(str(tmp_path))
     text = "<|im_start|>assistant\nhello world<|im_end|>\n"
     ids = proc(text=text)["input_ids"]
     assert ids.shape[0] == 1 and ids[0].tolist() == hf(text)["input_ids"]
     assert ids[0, 0].item() == hf.convert_tokens_to_ids("<|im_start|>")
-    assert isinstance(load_processor(str(tmp_path / "missing")), FallbackProcessor)
+    # the stand-in is reserved for the packaged synthetic presets; a real checkpoint dir without tokenizer
+    # files is an error, not a silent hash tokenizer
+    from qwen_tts.weights import resolve_path
+    import pytest
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        assert isinstance(load_processor(resolve_path("synthetic:tiny-customvoice")), FallbackProcessor)
+    (tmp_path / "ckpt").mkdir()
+    with pytest.raises(FileNotFoundError, match="tokenizer"):
+        load_processor(str(tmp_path / "ckpt"))
+
+
+def test_hub_ids_map_to_matching_presets():
+    """Every hub id resolves to a preset of its own size and model type (0.6B-Base is not the 1.7B preset)."""
+    import json
+    import warnings
+    from qwen_tts.weights import HUB_ALIASES, resolve_path
+    for hub in HUB_ALIASES:
+        if "tokenizer" in hub:
+            continue
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            d = resolve_path(hub)
+        cfg = json.load(open(os.path.join(d, "config.json")))
+        size = "0b6" if "0.6b" in hub else "1b7"
+        mtype = {"customvoice": "custom_voice", "voicedesign": "voice_design", "base": "base"}[hub.rsplit("-", 1)[1]]
+        assert cfg["tts_model_size"] == size and cfg["tts_model_type"] == mtype, hub
+        assert cfg["talker_config"]["hidden_size"] == (1024 if size == "0b6" else 2048), hub
+        if mtype == "base":
+            assert cfg["speaker_encoder_config"]["enc_dim"] == cfg["talker_config"]["hidden_size"], hub

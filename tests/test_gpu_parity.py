@@ -595,6 +595,39 @@ def test_sample_top_p_large_vocab(V):
         assert int(t[r]) in set(idx[r][keep[r]].tolist())
 
 
+@pytest.mark.parametrize("V,k,p", [(2048, 100, 1.0), (3072, 0, 0.9), (2048, 300, 0.95)])
+def test_sample_draw_at_total_stays_in_kept_set(V, k, p):
+    """Slow path (top_k > 64 or top_p < 1): a draw u that rounds to the total mass (forced via debug_u = 1.0) is
+    claimed by the last thread holding mass -- the last kept token in category order -- never token 0 or a token
+    outside the kept set, also when the block's last thread holds no mass."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    R = 16
+    g = torch.Generator().manual_seed(V + k)
+    logits = torch.randn(R, V, generator=g) * 2
+    logits[:, 0] = -30.0  # token 0 is never in the kept set
+    logits[:, 255::256] = -40.0  # thread 255's tokens: outside the kept set (that thread holds no mass)
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits.to(dev), R, V, V, tok, do_sample=True, top_k=k, top_p=p, temperature=1.0, seed=1,
+              step=torch.zeros(1, dtype=torch.int32, device=dev), substep=0, debug_u=1.0)
+    t = tok.cpu().long()
+    for r in range(R):
+        row = logits[r]
+        kept = torch.ones(V, dtype=torch.bool)
+        if 0 < k < V:
+            kept &= row >= torch.topk(row, k).values[-1]
+        if p < 1.0:
+            pr = torch.softmax(torch.where(kept, row, torch.tensor(-float("inf"))), -1)
+            sp, idx = pr.sort(descending=True)
+            keep = (sp.cumsum(-1) - sp) < p
+            kept &= torch.zeros(V, dtype=torch.bool).scatter(0, idx[keep], True)
+        # category order of the inverse CDF: thread-major (token v lives on thread v % 256, slot v // 256)
+        order = sorted(range(V), key=lambda v: (v % 256, v // 256))
+        last = [v for v in order if kept[v]][-1]
+        assert int(t[r]) != 0 and bool(kept[t[r]]), (r, int(t[r]))
+        assert int(t[r]) == last, (r, int(t[r]), last)
+
+
 # ------------------------------------------------------------------------------------------ end-to-end talker
 @pytest.fixture(scope="module")
 def tiny_models():
@@ -614,7 +647,8 @@ def _run_case(model, key, case, idx, cfg, use_graph=True):
     ids, ins, vcp, ref_ids = make_inputs(case, idx, cfg["talker_config"]["hidden_size"])
     return model.generate(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp,
                           languages=case["languages"], speakers=case["speakers"],
-                          non_streaming_mode=case["non_streaming_mode"], use_graph=use_graph, **gen_kwargs(case))
+                          non_streaming_mode=case["non_streaming_mode"], use_graph=use_graph, seed=case.get("seed"),
+                          **gen_kwargs(case))
 
 
 @pytest.mark.parametrize("use_graph", [True, False])
@@ -655,6 +689,8 @@ def test_checkpoint_directory_drop_in(tiny_models, tmp_path):
     _, ccfg = load_preset("tiny-customvoice")
     CW = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
     save_file(CW, str(tmp_path / "speech_tokenizer" / "model.safetensors"))
+    from cases import write_test_tokenizer
+    write_test_tokenizer(tmp_path)  # a real checkpoint dir carries its BPE files (no hash stand-in outside presets)
     tts = Qwen3TTSModel.from_pretrained(str(tmp_path), dtype=torch.float32)
     z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
     cases = talker_cases()
@@ -775,6 +811,74 @@ def test_stream_matches_one_shot(tiny_models, ctx, eos, frames):
         np.testing.assert_allclose(first, w[:first.shape[0]], atol=2e-4, rtol=0)
         if ctx >= 1000:
             np.testing.assert_allclose(got, w, atol=2e-4, rtol=0)
+
+
+def test_sampling_fresh_seed_per_call_reuses_session(tiny_models):
+    """Sampling draws a fresh Philox key per generate() call (like the reference's torch.multinomial): two calls
+    give different codes, torch.manual_seed reproduces a call, an explicit seed reproduces itself -- and every
+    call replays the same Session and captured graph (the seed is a device word, not part of the session key)."""
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype="fp32")
+    case = dict(talker_cases()["cv_b3_auto_nospk"], do_sample=True, subtalker_dosample=True, max_new_tokens=20)
+    a, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
+    sess = model.engine.all_sessions()
+    assert len(sess) == 1 and not sess[0].busy
+    graph = sess[0].graph
+    b, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
+    assert any(not torch.equal(x, y) for x, y in zip(a, b)), "two unseeded calls drew the same codes"
+    torch.manual_seed(123)
+    c, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
+    torch.manual_seed(123)
+    d, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
+    assert all(torch.equal(x, y) for x, y in zip(c, d))
+    e, _ = _run_case(model, "cv_b3_auto_nospk", dict(case, seed=77), 2, cfg)
+    f, _ = _run_case(model, "cv_b3_auto_nospk", dict(case, seed=77), 2, cfg)
+    assert all(torch.equal(x, y) for x, y in zip(e, f))
+    assert model.engine.all_sessions() == sess and sess[0].graph is graph  # no re-allocation, no re-capture
+
+
+def test_interleaved_streams_do_not_share_state(tiny_models):
+    """Two stream() generators of the same shape, advanced alternately (a server interleaving requests): each
+    gets a session of its own, and each one's PCM equals its one-shot generate() + decode()."""
+    from cases import gen_kwargs, make_inputs, talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype="fp32")
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    tok = Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer", dtype="fp32", weights=CW)
+    model.load_speech_tokenizer(tok)
+    key = "cv_b2_stream_dialect"
+    case = dict(talker_cases()[key], max_new_tokens=30)
+    kws, refs = [], []
+    for idx, spk in ((3, ["eric", "ryan"]), (11, ["ryan", "eric"])):  # different requests of one batch shape
+        ids, ins, vcp, ref_ids = make_inputs(case, idx, cfg["talker_config"]["hidden_size"])
+        kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp,
+                  languages=case["languages"], speakers=spk,
+                  non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+        codes, _ = model.generate(**kw)
+        refs.append(tok.decode([{"audio_codes": c} for c in codes])[0])
+        kws.append(kw)
+    assert not np.array_equal(refs[0][0], refs[1][0])
+    gens = [model.stream(first_chunk_frames=3, chunk_frames=4, **kw) for kw in kws]
+    chunks = [{}, {}]
+    live = [True, True]
+    while any(live):
+        for i, gnr in enumerate(gens):
+            if live[i]:
+                try:
+                    b, pcm, last = next(gnr)
+                    chunks[i].setdefault(b, []).append(pcm.cpu().numpy())
+                except StopIteration:
+                    live[i] = False
+    assert len(model.engine.all_sessions()) >= 2 and not any(s.busy for s in model.engine.all_sessions())
+    for i in range(2):
+        for b, w in enumerate(refs[i]):
+            np.testing.assert_allclose(np.concatenate(chunks[i][b]), w, atol=2e-4, rtol=0, err_msg=f"stream {i} row {b}")
 
 
 def test_talker_bf16_runs_and_tracks_fp32(tiny_models):

@@ -23,7 +23,7 @@ CASES = [("tiny-base", "tiny", "frontend_tiny.npz"), ("1.7b-base", "full", "fron
 
 def test_frontend_param_specs_match_reference():
     specs = json.load(open(os.path.join(GOLD, "param_specs.json")))
-    for p in ("tiny-base", "1.7b-base", "1.7b-customvoice"):
+    for p in ("tiny-base", "1.7b-base", "0.6b-base", "1.7b-customvoice"):
         cfg, ccfg = load_preset(p)
         assert {k: list(v) for k, v in encoder_param_specs(ccfg)} == specs[p + "/encoder"]
         if p.endswith("base"):

@@ -29,7 +29,7 @@ def tiny_talkers():
 
 def test_param_specs_match_reference():
     specs = json.load(open(os.path.join(GOLD, "param_specs.json")))
-    for p in ("tiny-customvoice", "1.7b-customvoice", "0.6b-customvoice"):
+    for p in ("tiny-customvoice", "1.7b-customvoice", "0.6b-customvoice", "0.6b-base"):
         cfg, ccfg = load_preset(p)
         ref = {k: v for k, v in specs[p].items() if not k.startswith("speaker_encoder")}
         assert {k: list(v) for k, v in talker_param_specs(cfg)} == ref
