@@ -52,14 +52,16 @@ def make_weights(preset, dev, world, rank):
     return cfg, W, CW
 
 
-ROOF_KERNEL = "gemv_wt<bf16,f32,bf16,WPB=4,U=4,rms,fold=2> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
+ROOF_KERNEL = "gemv_wt<bf16,bf16,bf16,WPB=4,U=4,rms,fold=2> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
 
 
 def gateup_bytes(eng, B):
-    """Algorithmic HBM bytes of one talker gate-up launch: bf16 weight tiles + fp32 A rows + bf16 SwiGLU out."""
+    """Algorithmic HBM bytes of one talker gate-up launch: bf16 weight tiles + A rows (the bf16 residual shadow in
+    bf16 mode) + bf16 SwiGLU out."""
     t = eng.talker
     L = t.layers[0].gu
-    return L.w.numel() * L.w.element_size() + B * t.H * 4 + B * t.I * 2
+    a_bytes = 2 if eng.wdt == torch.bfloat16 else 4
+    return L.w.numel() * L.w.element_size() + B * t.H * a_bytes + B * t.I * L.w.element_size()
 
 
 def kernel_roofline(tts, B, reps=10):
@@ -70,7 +72,7 @@ def kernel_roofline(tts, B, reps=10):
     eng = tts.model.engine
     t = eng.talker
     dev = eng.dev
-    x = torch.randn(B, t.H, device=dev)
+    x = torch.randn(B, t.H, device=dev).to(eng.wdt)  # production A: the bf16 residual shadow (fp32 in fp32 mode)
     h = torch.empty(B, t.I, dtype=eng.wdt, device=dev)
 
     def run():
@@ -259,9 +261,9 @@ def main():
     if a.roofline and rank == 0:
         r = kernel_roofline(tts, B)
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "r01_pmc_gateup.json")
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        pmcs = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_gateup.json"))
+        if pmcs:  # the newest round's PMC traffic of this kernel (tools/pmc_gateup.py + tools/pmc_reduce.py)
+            traffic = json.load(open(os.path.join(REPO, "profiles", pmcs[-1]))).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),

@@ -73,6 +73,10 @@ typedef struct qt_gemm_args {
   /* QT_AACT_ELU: ELU(alpha = 1) on every A element (zero padding stays zero) -- the nn.ELU that precedes every
    * MimiConv1d of the tokenizer encoder (transformers modeling_mimi.py MimiEncoder / MimiResnetBlock) */
   int a_act;
+  /* optional bf16 copy of every element the epilogue stores (fp32 out, QT_EPI_STORE / QT_EPI_ADD, M <= 16):
+   * out2[m*ldo2 + n] = bf16(out[m*ldo + n]).  Decode writes the residual stream this way so the next
+   * RMS-normalised GEMV reads its A operand at half the bytes (its MFMA rounds A to bf16 anyway). */
+  void* out2; long long ldo2;
 } qt_gemm_args;
 #define QT_GEMM_WS_MIN (4 << 20)
 
@@ -162,6 +166,7 @@ typedef struct qt_attn_oproj_args {
   void* k_cache; void* v_cache; int kv_dtype;
   const void* w_o; int w_dtype; int N;
   float* x; long long ldx;
+  void* x16; long long ldx16;  /* optional bf16 copy of the updated residual rows (next RMS GEMV's A operand) */
 } qt_attn_oproj_args;
 int qt_decode_attn_oproj(const qt_attn_oproj_args* args, void* stream);
 
@@ -212,6 +217,7 @@ typedef struct qt_sample_args {
    * request without recapture); NULL -> `seed` above */
   const unsigned long long* seed_ptr;
   float debug_u;  /* < 0: off.  Tests only: replaces the unit uniform of the inverse-CDF draw (1.0 -> u = total) */
+  void* emb_out16; long long emb_ld16;  /* optional bf16 copy of the emb_out row (next RMS-normalised GEMV's A) */
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 
@@ -226,10 +232,11 @@ int qt_rmsnorm_rec(const float* x, const float* gamma, float eps, float* out, in
 int qt_gather_rows(const void* table, int dtype, const int* idx, int M, int H, float* out, long long ldo, void* stream);
 
 /* Talker decode input (M:1681-1692): x[b] = E0[codes[b,t,0]] + sum_g Ecp[g][codes[b,t,1+g]]
- * + (t < T ? trailing[b][t] : pad).  codes: int32 [B][codes_ld] rows holding [F][G]. */
+ * + (t < T ? trailing[b][t] : pad).  codes: int32 [B][codes_ld] rows holding [F][G].  x16 (optional):
+ * bf16 copy of x ([B][H]), the A operand of the first layer's RMS-normalised QKV GEMV. */
 int qt_frame_embed(const void* emb0, const void* emb_cp, int dtype, int V0, int Vcp, int G, int H,
                    const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
-                   const float* pad, float* x, int B, void* stream);
+                   const float* pad, float* x, void* x16, int B, void* stream);
 
 /* counters[i] += 1 for i < n (end-of-frame step / position advance inside a captured graph). */
 int qt_advance(int* counters, int n, void* stream);

@@ -873,6 +873,7 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
     float v = 0.f;
     for (int h = 0; h < nk; ++h) v += red[h][lane >> 4][lane & 15];
     p.x[(long long)r * p.ldx + col] = xres + v;
+    if (p.x16) ((bf16_t*)p.x16)[(long long)r * p.ldx16 + col] = f2bf(xres + v);
   }
 }
 

@@ -35,8 +35,8 @@ struct GemmP {
   unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
   const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
   int a_elu;                    // ELU on A (tokenizer encoder convs)
-  int dbg;                      // measurement hook of the decode GEMV (QT_GEMV_DBG): 1 = no A loads, 2 = no MFMA
   int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))
+  bf16_t* out2; long long ldo2; // optional bf16 copy of the stored output (decode residual stream shadow)
 };
 
 // SnakeBeta exactly as qt_snake computes it (fp32 math on the stored activation)
@@ -189,8 +189,9 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
     const int m = m0 + mt * 16 + lk * 4 + i;
     if (m >= p.M || !nval) continue;
     OT* o = out + (long long)m * p.ldo + n;
-    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(to_f(*o) + v[i]);
-    else *o = from_f<OT>(v[i]);
+    const float r = p.epi == QT_EPI_ADD ? to_f(*o) + v[i] : v[i];
+    *o = from_f<OT>(r);
+    if (p.out2) p.out2[(long long)m * p.ldo2 + n] = f2bf(r);
   }
 }
 
@@ -206,6 +207,23 @@ __global__ __launch_bounds__(WPB * 64) void gemm_wt(GemmP p) {
 // few-column-tile GEMV gets more blocks without a cross-block split-K reduction (its weight tiles are re-read
 // from L2 by the z blocks; blockIdx.x-major launch keeps a tile's row blocks ntiles apart, same XCD when
 // ntiles % 8 == 0).
+// Loads hipcc does not track (see gemv_wt's epilogue prefetch): the destination is only read after an
+// asm_wait that names it "+v", so the compiler never reads it before the data has landed.
+QT_DEV unsigned asm_load_b32(const void* ptr) {
+  unsigned v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
+QT_DEV unsigned asm_load_raw(const float* ptr) { return asm_load_b32(ptr); }
+QT_DEV unsigned asm_load_raw(const bf16_t* ptr) {
+  unsigned v;
+  asm volatile("global_load_ushort %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
+template <typename T> QT_DEV float raw_to_f(unsigned u);
+template <> QT_DEV float raw_to_f<float>(unsigned u) { return __uint_as_float(u); }
+template <> QT_DEV float raw_to_f<bf16_t>(unsigned u) { return __uint_as_float(u << 16); }
+
 // DPP row_ror:S on each dword of a 16-byte fragment (rotate right: lane l of a 16-lane row receives lane
 // (l - S) mod 16)
 template <int S>
@@ -239,22 +257,33 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   const int hsel = lm / RPF;    // which k tile of the fold group it fetches
   const bool rowok = arow_i < mr;
   const int mrow = m0 + (rowok ? arow_i : mr - 1);
-  const AT* arow = (const AT*)p.A + (p.a_index ? (long long)p.a_index[mrow] : (long long)mrow) * p.lda + lk * E;
+  // gathered row (a_index): an untracked load waited for here, so no compiler-visible load is pending at the chunk
+  // loop's preheader (hipcc flushes those with a vmcnt(0) that would also wait for the epilogue prefetch)
+  unsigned grow = (unsigned)mrow;
+  if (p.a_index) {
+    grow = asm_load_b32(p.a_index + mrow);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(grow)::"memory");
+  }
+  const AT* arow = (const AT*)p.A + (long long)(int)grow * p.lda + lk * E;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   float ssv[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) ssv[i] = 0.f;
-  // epilogue operands of wave 0 issued before the weight stream (hides one dependent round trip)
+  // epilogue operands of wave 0 issued before the weight stream (hides one dependent round trip).  Inline-asm loads
+  // (waited for by asm_wait_epi below): hipcc would otherwise flush them with a vmcnt(0) at the chunk loop's
+  // preheader, i.e. wait a full round trip before issuing the first weight fragment.
   const int n = nt * 16 + lm;
   const bool nval = n < p.N;
-  float pre_bias = 0.f, pre_cs = 1.f, pre_out[4] = {0.f, 0.f, 0.f, 0.f};
-  if (w == 0) {
-    if (p.bias && nval) pre_bias = p.bias[n];
-    if (p.colscale && nval) pre_cs = p.colscale[n];
-    if (p.epi == QT_EPI_ADD && nval) {
+  const int nc = min(n, p.N - 1);  // clamped column: every lane loads, no per-load branch
+  unsigned pre_bias = 0u, pre_cs = 0u, pre_out[4] = {0u, 0u, 0u, 0u};
+  const bool pre = w == 0;
+  if (pre) {
+    if (p.bias) pre_bias = asm_load_b32(p.bias + nc);
+    if (p.colscale) pre_cs = asm_load_b32(p.colscale + nc);
+    if (p.epi == QT_EPI_ADD) {
+      const OT* ob = (const OT*)p.out + nc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (lk * 4 + i < mr) pre_out[i] = to_f(((const OT*)p.out)[(long long)(m0 + lk * 4 + i) * p.ldo + n]);
+      for (int i = 0; i < 4; ++i) pre_out[i] = asm_load_raw(ob + (long long)(m0 + min(lk * 4 + i, mr - 1)) * p.ldo);
     }
   }
   const WT* wp = (const WT*)p.W + ((size_t)nt * ktiles) * 64 * E + lane * E;
@@ -274,11 +303,10 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     for (int q = 0; q < NA; ++q) {
       // every lane loads (with F == 1, rows >= M re-fetch row M-1 from L2: predicating the load on the row was
       // measured slower, profiles/r01_gemv_variants_ab.jsonl)
+      // (no runtime branch around these loads: hipcc then waits vmcnt(0) after each one, serialising the chunk's
+      // round trips -- tools/gemv_probe.hip)
       const int kc = min(c + F * q + hsel, kt1 - 1);
-      if (p.dbg & 1) {
-#pragma unroll
-        for (int i = 0; i < E; ++i) a[q][i] = 1.f;
-      } else if constexpr (E == 8) load8f(arow + kc * KT, a[q]); else load4f(arow + kc * KT, a[q]);
+      if constexpr (E == 8) load8f(arow + kc * KT, a[q]); else load4f(arow + kc * KT, a[q]);
     }
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
@@ -289,9 +317,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
         if constexpr (NORM) ssv[i] += x * x;  // E independent chains (not one 4*U*E-long chain)
         a[q][i] = x;
       }
-      if (p.dbg & 2) {
-        acc[0] += __uint_as_float(wv[q][0] ^ wv[q][1] ^ wv[q][2] ^ wv[q][3]) + a[q][0];
-      } else if constexpr (F > 1) {
+      if constexpr (F > 1) {
         const u32x4_t own = {pack2bf(a[q][0], a[q][1]), pack2bf(a[q][2], a[q][3]), pack2bf(a[q][4], a[q][5]),
                              pack2bf(a[q][6], a[q][7])};
         const u32x4_t zero = {0u, 0u, 0u, 0u};
@@ -332,6 +358,9 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
+  // the epilogue prefetch has landed (it was issued before every weight load the loop waited for)
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(pre_bias), "+v"(pre_cs), "+v"(pre_out[0]), "+v"(pre_out[1]), "+v"(pre_out[2]),
+               "+v"(pre_out[3])::"memory");
   float v[4] = {0.f, 0.f, 0.f, 0.f}, ssr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ww = 0; ww < WPB; ++ww) {
@@ -386,7 +415,8 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
       }
     }
   }
-  const float bias = pre_bias, cs = pre_cs;
+  const float bias = (p.bias && nval) ? __uint_as_float(pre_bias) : 0.f;
+  const float cs = (p.colscale && nval) ? __uint_as_float(pre_cs) : 1.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float x = v[i];
@@ -411,8 +441,9 @@ __global__ __launch_bounds__(WPB * 64) void gemv_wt(GemmP p) {
     const int m = lk * 4 + i;
     if (m >= mr || !nval) continue;
     OT* o = out + (long long)(m0 + m) * p.ldo + n;
-    if (p.epi == QT_EPI_ADD) *o = from_f<OT>(pre_out[i] + v[i]);
-    else *o = from_f<OT>(v[i]);
+    const float r = p.epi == QT_EPI_ADD ? raw_to_f<OT>(pre_out[i]) + v[i] : v[i];
+    *o = from_f<OT>(r);
+    if (p.out2) p.out2[(long long)(m0 + m) * p.ldo2 + n] = f2bf(r);
   }
 }
 
@@ -826,6 +857,8 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.A = a->A; p.lda = a->lda; p.a_index = a->a_index; p.W = a->W;
   p.gamma = a->gamma; p.eps = a->eps; p.rms = a->rmsnorm || a->gamma != nullptr; p.bias = a->bias; p.colscale = a->colscale;
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
+  p.out2 = (bf16_t*)a->out2; p.ldo2 = a->ldo2;
+  if (p.out2 && (a->M > 16 || a->taps > 0 || a->epi == QT_EPI_SWIGLU || a->o_dtype != QT_F32)) return QT_ERR_ARG;
   p.sn_a = a->snake_alpha; p.sn_ib = a->snake_inv_beta;
   if ((p.sn_a == nullptr) != (p.sn_ib == nullptr)) return QT_ERR_ARG;
   if (a->a_act != QT_AACT_NONE && a->a_act != QT_AACT_ELU) return QT_ERR_ARG;
@@ -833,8 +866,6 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.a_elu = a->a_act == QT_AACT_ELU;
   static const int no_ig = [] { const char* e = getenv("QT_NO_IGEMM"); return e ? atoi(e) : 0; }();
   p.no_igemm = no_ig;
-  static const int dbg = [] { const char* e = getenv("QT_GEMV_DBG"); return e ? atoi(e) : 0; }();
-  p.dbg = dbg;
   // weights streamed once per frame (talker-size matrices) bypass cache retention so the re-read code-predictor
   // weights stay in L2 / Infinity Cache; QT_GEMV_NT=0/1 forces it off/on for every decode GEMV (measurement)
   static const int nt_env = [] { const char* e = getenv("QT_GEMV_NT"); return e ? atoi(e) : -1; }();

@@ -39,7 +39,8 @@ __global__ __launch_bounds__(256) void frame_embed_k(const ET* __restrict__ e0, 
                                                      int Vcp, int G, int H, const int* __restrict__ codes,
                                                      long long codes_ld, const int* __restrict__ step,
                                                      const float* __restrict__ trailing, int T,
-                                                     const float* __restrict__ pad, float* __restrict__ x) {
+                                                     const float* __restrict__ pad, float* __restrict__ x,
+                                                     bf16_t* __restrict__ x16) {
   // ET: table dtype.  Codes to LDS once, then every thread issues its 16 row-slice loads before summing.
   __shared__ int cs[32];
   const int b = blockIdx.x;
@@ -60,6 +61,9 @@ __global__ __launch_bounds__(256) void frame_embed_k(const ET* __restrict__ e0, 
     for (int j = 0; j < 8; ++j) acc[j] += v[j];
     store4(x + (long long)b * H + i, acc);
     store4(x + (long long)b * H + i + 4, acc + 4);
+    if (x16)
+      *(u32x4_t*)(x16 + (long long)b * H + i) =
+          u32x4_t{pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]), pack2bf(acc[4], acc[5]), pack2bf(acc[6], acc[7])};
   }
 }
 
@@ -176,14 +180,14 @@ extern "C" int qt_gather_rows(const void* tab, int dtype, const int* idx, int M,
 
 extern "C" int qt_frame_embed(const void* e0, const void* ecp, int dtype, int V0, int Vcp, int G, int H,
                               const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
-                              const float* pad, float* x, int B, void* s) {
+                              const float* pad, float* x, void* x16, int B, void* s) {
   if (B <= 0 || H <= 0 || G < 1 || G > 32 || H % 8) return QT_ERR_SHAPE;
   if (dtype == QT_BF16)
     hipLaunchKernelGGL(frame_embed_k<bf16_t>, dim3(B), dim3(256), 0, (hipStream_t)s, (const bf16_t*)e0,
-                       (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x);
+                       (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
   else if (dtype == QT_F32)
     hipLaunchKernelGGL(frame_embed_k<float>, dim3(B), dim3(256), 0, (hipStream_t)s, (const float*)e0,
-                       (const float*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x);
+                       (const float*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
   else
     return QT_ERR_DTYPE;
   return ok();

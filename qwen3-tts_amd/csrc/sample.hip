@@ -448,7 +448,12 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   if (p.emb_table) {  // next-step input row: the chosen token's (projected) embedding
     const float* src = p.emb_table + (long long)tok * p.emb_dim;
     float* dst = p.emb_out + (long long)r * p.emb_ld;
-    for (int i = tid * 4; i < p.emb_dim; i += NT * 4) *(f32x4_t*)(dst + i) = *(const f32x4_t*)(src + i);
+    bf16_t* d16 = p.emb_out16 ? (bf16_t*)p.emb_out16 + (long long)r * p.emb_ld16 : nullptr;
+    for (int i = tid * 4; i < p.emb_dim; i += NT * 4) {
+      const f32x4_t v = *(const f32x4_t*)(src + i);
+      *(f32x4_t*)(dst + i) = v;
+      if (d16) *(uint2*)(d16 + i) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    }
   }
   if (tid != 0) return;
   p.tok_out[r] = tok;
@@ -466,6 +471,7 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * 16 || !a->tok_out) return QT_ERR_SHAPE;
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
+  if (a->emb_out16 && (!a->emb_table || a->emb_ld16 % 4)) return QT_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
   const SK k{*a, stop};

@@ -32,7 +32,8 @@ class GemmArgs(ctypes.Structure):
                 ("out", c_void_p), ("ldo", c_ll), ("taps", c_int), ("dil", c_int), ("cin", c_int),
                 ("cin_pad", c_int), ("t_in", c_int), ("t_out", c_int), ("t_off", c_int),
                 ("ws", c_void_p), ("ws_bytes", c_ll), ("splitk", c_int),
-                ("snake_alpha", c_void_p), ("snake_inv_beta", c_void_p), ("a_act", c_int)]
+                ("snake_alpha", c_void_p), ("snake_inv_beta", c_void_p), ("a_act", c_int),
+                ("out2", c_void_p), ("ldo2", c_ll)]
 
 GEMM_WS_MIN = 4 << 20  # QT_GEMM_WS_MIN
 
@@ -65,7 +66,7 @@ class AttnOprojArgs(ctypes.Structure):
                 ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float), ("cos_tab", c_void_p), ("sin_tab", c_void_p),
                 ("rope_pos", c_void_p), ("kv_pos", c_void_p), ("row_start", c_void_p), ("const_pos", c_int),
                 ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int), ("w_o", c_void_p), ("w_dtype", c_int),
-                ("N", c_int), ("x", c_void_p), ("ldx", c_ll)]
+                ("N", c_int), ("x", c_void_p), ("ldx", c_ll), ("x16", c_void_p), ("ldx16", c_ll)]
 
 
 class SampleArgs(ctypes.Structure):
@@ -77,7 +78,7 @@ class SampleArgs(ctypes.Structure):
                 ("tok_out", c_void_p), ("codes", c_void_p), ("codes_ld", c_ll), ("codes_w", c_int),
                 ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int),
                 ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll),
-                ("seed_ptr", c_void_p), ("debug_u", c_float)]
+                ("seed_ptr", c_void_p), ("debug_u", c_float), ("emb_out16", c_void_p), ("emb_ld16", c_ll)]
 
 
 class MlpArgs(ctypes.Structure):
@@ -110,7 +111,7 @@ def load_library(path: str = LIB_PATH):
         "qt_rmsnorm_rec": [P, P, c_float, P, c_int, c_int, P, c_ll, P, c_int, P],
         "qt_small_prefill_attention": [P, c_int, P],
         "qt_gather_rows": [P, c_int, P, c_int, c_int, P, c_ll, P],
-        "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, c_int, P],
+        "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, P, c_int, P],
         "qt_advance": [P, c_int, P],
         "qt_rvq_gather": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P],
         "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],

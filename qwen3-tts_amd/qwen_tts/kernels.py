@@ -140,10 +140,11 @@ class use_workspace:
 
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
          act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0, snake=None,
-         a_act=_hip.AACT_NONE):
+         a_act=_hip.AACT_NONE, out2=None, ldo2=None):
     """conv = (t_in, t_out, t_off, dil) for implicit-conv weights.  splitk: 0 auto, 1 off, n forced
     (decode GEMV only, needs gemm_workspace(device) allocated).  snake = (alpha, inv_beta): SnakeBeta applied
-    to A per input channel inside the GEMM (fused codec activation)."""
+    to A per input channel inside the GEMM (fused codec activation).  out2: bf16 copy of the stored fp32 output
+    (M <= 16; the decode residual stream's shadow read by the next RMS-normalised GEMV)."""
     a = _hip.GemmArgs()
     a.M, a.N, a.K = M, W.N, W.K
     a.a_dtype = _hip.dtype_code(a_dtype or A.dtype)
@@ -157,6 +158,8 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     if snake is not None:
         a.snake_alpha, a.snake_inv_beta = ptr(snake[0]), ptr(snake[1])
     a.a_act = a_act
+    if out2 is not None:
+        a.out2, a.ldo2 = ptr(out2), ldo if ldo2 is None else ldo2
     ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
     if ws is not None and M <= 16 and not W.taps:
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
@@ -236,8 +239,9 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
 
 
 def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc, Lmax, w_o: "Tiled", x, *,
-                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None):
-    """qt_decode_attn_oproj: x[:R] += o_proj(decode attention) in one launch (row r = batch entry r, short caches)."""
+                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None, x16=None):
+    """qt_decode_attn_oproj: x[:R] += o_proj(decode attention) in one launch (row r = batch entry r, short caches).
+    x16: bf16 shadow of x, updated alongside."""
     a = _hip.AttnOprojArgs()
     a.R, a.Hq, a.Hkv, a.D, a.Lmax = R, Hq, Hkv, D, Lmax
     a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
@@ -246,14 +250,17 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
     a.k_cache, a.v_cache, a.kv_dtype = ptr(kc), ptr(vc), _hip.dtype_code(kc.dtype)
     a.w_o, a.w_dtype, a.N = ptr(w_o.w), _hip.dtype_code(w_o.dtype), w_o.N
     a.x, a.ldx = ptr(x), x.stride(0)
+    if x16 is not None:
+        a.x16, a.ldx16 = ptr(x16), x16.stride(0)
     check(_hip.lib().qt_decode_attn_oproj(ctypes.byref(a), stream()), "qt_decode_attn_oproj")
 
 
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
-           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0):
-    """emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r].
+           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None):
+    """emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
+    emb16 = (out bf16 rows, ld): its bf16 copy.
     seed_ptr: device int64 [1] read at run time instead of `seed` (graph-captured samplers)."""
     a = _hip.SampleArgs()
     a.logits, a.R, a.V, a.ld = ptr(logits), R, V, ld
@@ -268,6 +275,8 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     a.seed_ptr, a.debug_u = ptr(seed_ptr), float(debug_u)
     if emb is not None:
         a.emb_table, a.emb_dim, a.emb_out, a.emb_ld = ptr(emb[0]), emb[0].shape[1], ptr(emb[1]), emb[2]
+        if emb16 is not None:
+            a.emb_out16, a.emb_ld16 = ptr(emb16[0]), emb16[1]
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 
@@ -285,9 +294,10 @@ def gather_rows(table, idx, M, H, out, ldo):
           "qt_gather_rows")
 
 
-def frame_embed(e0, ecp, G, H, codes, codes_ld, step, trailing, T, pad, x, B):
+def frame_embed(e0, ecp, G, H, codes, codes_ld, step, trailing, T, pad, x, B, x16=None):
     check(_hip.lib().qt_frame_embed(ptr(e0), ptr(ecp), _hip.dtype_code(e0.dtype), e0.shape[0], ecp.shape[1], G, H,
-                                    ptr(codes), codes_ld, ptr(step), ptr(trailing), T, ptr(pad), ptr(x), B, stream()),
+                                    ptr(codes), codes_ld, ptr(step), ptr(trailing), T, ptr(pad), ptr(x), ptr(x16), B,
+                                    stream()),
           "qt_frame_embed")
 
 

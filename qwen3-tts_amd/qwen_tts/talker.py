@@ -63,17 +63,24 @@ class _Stack:
         if self.cos.shape[0] < npos:
             self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
 
-    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False):
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None):
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
-        decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention."""
+        decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention.
+        x16 (bf16 mode, R <= 16): bf16 shadow of x, kept current by every writer of x (the residual-add epilogues
+        store both) and read as the A operand of the RMS-normalised GEMVs (QKV, gate/up): their MFMA rounds A to
+        bf16 anyway, so only the RMS row sums change (they come from the bf16 values, as the reference's bf16
+        residual stream gives them) while the activation fetch halves."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
+        if x16 is not None and ("mlp_ws" in scratch or R > 16):
+            x16 = None  # the fused MLP / prefill GEMMs write x only
+        xa = x if x16 is None else x16
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            K.gemm(x, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
+            K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
-                                    self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"])
+                                    self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"], x16=x16)
             elif decode:
                 K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                    self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
@@ -87,12 +94,12 @@ class _Stack:
                 K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             if not fused_ao:
-                K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD)
+                K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD, out2=x16)
             if "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
                 K.mlp_decode(x, R, self.H, self.I, L.gu, L.down, self.eps, scratch["mlp_ws"], scratch["mlp_err"])
             else:
-                K.gemm(x, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
-                K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD)
+                K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
+                K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD, out2=x16)
 
 
 # qt_mlp_decode (one-launch MLP) is correct and tested but measured slower than the two GEMVs on MI355X
@@ -102,6 +109,8 @@ FUSED_MLP = os.environ.get("QT_FUSED_MLP", "0") == "1"
 # code-predictor decode steps: qt_decode_attn_oproj (attention fused into o_proj + residual); QT_ATTN_OPROJ=0 keeps
 # the two-launch path (decode attention, then the o_proj GEMV) for A/B measurement
 ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
+# bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
+X16 = os.environ.get("QT_X16", "1") == "1"
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -138,6 +147,7 @@ class CPLane:
         i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
         # prefill rows (2r, 2r + 1) = (past_hidden, cb0 embedding); decode rows 0..nb-1 of the same slice
         self.x = s.cp_x[2 * b0:2 * b1]
+        self.x16 = None if s.cp_x16 is None else s.cp_x16[2 * b0:2 * b1]
         self.kv = ([k[b0:b1] for k in s.cp_kv[0]], [v[b0:b1] for v in s.cp_kv[1]])
         self.sc = _scratch(2 * nb, c, dev, attn_oproj=True)
         self.ws = ws
@@ -210,6 +220,11 @@ class Session:
                      "row_batch": torch.arange(B, dtype=torch.int32, device=dev)}
         f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.x = f32(B, t.H)
+        # bf16 shadows of the decode residual streams (bf16 mode): A operands of the RMS-normalised GEMVs
+        use16 = eng.wdt == torch.bfloat16 and not FUSED_MLP and X16  # the fused MLP writes x only
+        bf = lambda *s: torch.zeros(*s, dtype=torch.bfloat16, device=dev) if use16 else None  # noqa: E731
+        self.x16 = bf(B, t.H)
+        self.cp_x16 = bf(2 * B, c.H)
         self.past_hidden = f32(B, t.H)
         self.logits = f32(B, eng.V)
         self.cp_x = f32(2 * B, c.H)
@@ -365,7 +380,8 @@ class TalkerEngine:
                  finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
                  temperature=gp.temperature, seed_ptr=s.seed, step=s.step, substep=substep, codes=s.codes,
                  codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off,
-                 row_base=s.row_base, emb=(self.cp_in_tab0, s.cp_x.view(-1)[self.cp.H:], 2 * self.cp.H))
+                 row_base=s.row_base, emb=(self.cp_in_tab0, s.cp_x.view(-1)[self.cp.H:], 2 * self.cp.H),
+                 emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[self.cp.H:], 2 * self.cp.H))
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
@@ -389,8 +405,8 @@ class TalkerEngine:
                 main.wait_stream(self._cp_streams[i - 1])
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
-                      s.trailing.shape[1], s.pad_embed, s.x, B)
-        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True)
+                      s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16)
+        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
         # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])
         K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
@@ -404,24 +420,29 @@ class TalkerEngine:
         # --- prefill: rows (2r, 2r+1) = (past_hidden[r], codec_embedding(tok0[r])); the odd rows were written by
         # the talker sampler that chose tok0 (projected embedding table)
         if self.s2m is not None:
-            K.gemm(s.past_hidden[ln.b0:ln.b1], self.s2m, ln.x, nb, t.H, 2 * Hc)
+            K.gemm(s.past_hidden[ln.b0:ln.b1], self.s2m, ln.x, nb, t.H, 2 * Hc, out2=ln.x16)
         else:
             ln.x.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
-        c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L)
-        self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0)
+            if ln.x16 is not None:
+                ln.x16.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
+        p16 = ln.x16 if 2 * nb <= 16 else None  # forward() keeps the shadow for decode-GEMV row counts only
+        c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
+        self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
-            c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True)
-            self._cp_head(s, ln, x, Hc, g)
+            x16 = None if ln.x16 is None else ln.x16[:nb]
+            c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16)
+            self._cp_head(s, ln, x, Hc, g, x16)
 
-    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g):
+    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None):
         c, gp = self.cp, s.gp
-        K.gemm(h, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
+        K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed_ptr=s.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
                  codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base + ln.b0,
-                 emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None)
+                 emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None,
+                 emb16=(ln.x16, c.H) if ln.x16 is not None and g < self.G - 2 else None)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,

@@ -19,7 +19,7 @@ W = synthetic(specs, dev)
 t = _Stack(W, "talker.model", tc, torch.bfloat16, dev, 64)
 del W
 B = 8
-x = torch.randn(B, t.H, device=dev)
+x = torch.randn(B, t.H, device=dev).to(torch.bfloat16)  # the bf16 residual shadow, as in the frame graph
 h = torch.empty(B, t.I, dtype=torch.bfloat16, device=dev)
 torch.cuda.synchronize()
 for _ in range(3):

@@ -18,11 +18,11 @@ def per_dispatch(d, counter):
 
 fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
 write = per_dispatch(sys.argv[2], "WRITE_SIZE")
-algo = 12288 * 2048 * 2 + 8 * 2048 * 4 + 8 * 6144 * 2
+algo = 12288 * 2048 * 2 + 8 * 2048 * 2 + 8 * 6144 * 2  # bf16 weights + bf16 A (residual shadow) + bf16 out
 f_kib = sum(fetch) / len(fetch)
 w_kib = sum(write) / len(write)
 hbm = 2 * f_kib * 1024 + w_kib * 1024
-out = {"kernel": "gemv_wt<bf16,f32,bf16,4,4,rms> talker gate-up, N=12288 K=2048 M=8",
+out = {"kernel": "gemv_wt<bf16,bf16,bf16,4,4,rms> talker gate-up, N=12288 K=2048 M=8",
        "dispatches": len(fetch), "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
        "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": algo,
        "traffic_over_algorithmic": round(hbm / algo, 4),
