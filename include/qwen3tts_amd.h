@@ -218,6 +218,9 @@ typedef struct qt_sample_args {
   const unsigned long long* seed_ptr;
   float debug_u;  /* < 0: off.  Tests only: replaces the unit uniform of the inverse-CDF draw (1.0 -> u = total) */
   void* emb_out16; long long emb_ld16;  /* optional bf16 copy of the emb_out row (next RMS-normalised GEMV's A) */
+  /* optional second gathered row (with emb_table): emb2_out[r*emb2_ld + i] = emb2_table[tok*emb2_dim + i] -- the
+   * code predictor's layer-0 q/k/v projection of every table row, precomputed, so the next step skips that GEMV */
+  const float* emb2_table; int emb2_dim; float* emb2_out; long long emb2_ld;
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 

@@ -645,109 +645,141 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
   const int ntiles = (p.N + 15) / 16, ktiles = nq * D / KT;
   const bool head = w < nk;  // this wave owns kv head w
 
-  // 1. weight fragments (column tiles cg*NT.., k tiles of head w), the residual row slice and the first batch of
-  // this head's cached keys: all issued before any dependent work
-  u32x4_t wv[NT][KTS];
-  if (head) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const WT* wp = (const WT*)p.w_o + ((size_t)min(cg * NT + t, ntiles - 1) * ktiles + (size_t)w * KTS) * 64 * E + lane * E;
-#pragma unroll
-      for (int kt = 0; kt < KTS; ++kt) wv[t][kt] = *(const u32x4_t*)(wp + (size_t)kt * 64 * E);
-    }
-  }
-  const int col = cg * NT * 16 + lane;
-  const float xres = (w == 0 && lane < NT * 16 && col < p.N) ? p.x[(long long)r * p.ldx + col] : 0.f;
+  // 1. every load of the prologue, issued in the order the phases need them -- this lane's q/k/v vector and its
+  // norm / RoPE parameters (phase 2), the first batch of cached keys (phase 3), the o_proj weight fragments (phase 4),
+  // the residual -- as inline-asm loads with counted waits: hipcc's own waits flush every outstanding load at each
+  // loop preheader, which made the q/k norm wait for the o_proj weights (the largest and last-needed bytes).
+  // Every wave issues the same loads (clamped head / row / column indices) so the counts hold in every wave.
+  const int hw = head ? w : 0;
   const int kvpos = CPOS ? p.const_pos : p.kv_pos[r];
   const int start = CPOS ? 0 : p.row_start[r];
+  const int pos = CPOS ? p.const_pos : p.rope_pos[r];
   const int nc = kvpos - start;  // cached keys [start, kvpos); the new key (kvpos) comes from LDS
-  const long long kvbase = ((long long)r * nk + (head ? w : 0)) * p.Lmax * D;
-  unsigned kr[IC][RW], vr[IC][RW];
-  auto load_batch = [&](int j0) {
-#pragma unroll
-    for (int c = 0; c < IC; ++c) {
-      const int jj = min(j0 + c * GPW + grp, max(nc - 1, 0));  // clamped (masked in the math)
-      const unsigned* ks = (const unsigned*)((const KV*)p.k_cache + kvbase + (long long)(start + jj) * D + sub * 8);
-      const unsigned* vs = (const unsigned*)((const KV*)p.v_cache + kvbase + (long long)(start + jj) * D + sub * 8);
-#pragma unroll
-      for (int q4 = 0; q4 < RW; q4 += 4) {
-        const u32x4_t a = *(const u32x4_t*)(ks + q4), b = *(const u32x4_t*)(vs + q4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { kr[c][q4 + e] = a[e]; vr[c][q4 + e] = b[e]; }
-      }
-    }
+  const int nvec = nq + 2 * nk;  // host-checked: nvec <= NW * GPW (one vector per lane group)
+  const int e0 = sub * 8, ec = e0 % half;
+  const int hh = w * GPW + grp;
+  const float* xsrc = p.qkv + (long long)r * nvec * D + (long long)min(hh, nvec - 1) * D + e0;
+  u32x4_t xq[2], qwr[2], kwr[2], cvr[2], svr[2];
+  {
+    const float* qn = p.q_norm ? p.q_norm + e0 : xsrc;
+    const float* kn_ = p.k_norm ? p.k_norm + e0 : xsrc;
+    const float* cs = p.cos_tab + (long long)pos * half + ec;
+    const float* sn = p.sin_tab + (long long)pos * half + ec;
+    asm_ld16(xq[0], xsrc); asm_ld16(xq[1], xsrc + 4);
+    asm_ld16(qwr[0], qn); asm_ld16(qwr[1], qn + 4);
+    asm_ld16(kwr[0], kn_); asm_ld16(kwr[1], kn_ + 4);
+    asm_ld16(cvr[0], cs); asm_ld16(cvr[1], cs + 4);
+    asm_ld16(svr[0], sn); asm_ld16(svr[1], sn + 4);
+  }
+  constexpr int RQ = RW / 4;  // 16-byte loads per key row slice
+  const long long kvbase = ((long long)r * nk + hw) * p.Lmax * D;
+  u32x4_t kq[IC][RQ], vq[IC][RQ];
+  auto kv_addr = [&](int j0, int c, bool isv) {
+    const int jj = min(j0 + c * GPW + grp, max(nc - 1, 0));  // clamped (masked in the math)
+    return (const KV*)(isv ? p.v_cache : p.k_cache) + kvbase + (long long)(start + jj) * D + sub * 8;
   };
-  if (head) load_batch(0);
-  if (pk.stop == 1) {
-    unsigned acc1 = kr[0][0];
-    if (head) {
 #pragma unroll
-      for (int kt = 0; kt < KTS; ++kt) acc1 ^= wv[0][kt][0];
+  for (int c = 0; c < IC; ++c)
+#pragma unroll
+    for (int q4 = 0; q4 < RQ; ++q4) {
+      asm_ld16(kq[c][q4], (const unsigned*)kv_addr(0, c, false) + 4 * q4);
+      asm_ld16(vq[c][q4], (const unsigned*)kv_addr(0, c, true) + 4 * q4);
     }
-    if (acc1 == 0x9E3779B9u && xres == 1234.5f) p.x[0] = 0.f;
+  u32x4_t wv[NT][KTS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const WT* wp = (const WT*)p.w_o + ((size_t)min(cg * NT + t, ntiles - 1) * ktiles + (size_t)hw * KTS) * 64 * E + lane * E;
+#pragma unroll
+    for (int kt = 0; kt < KTS; ++kt) asm_ld16(wv[t][kt], wp + (size_t)kt * 64 * E);
+  }
+  const int col = cg * NT * 16 + lane;
+  unsigned xres_u;
+  asm_ld4(xres_u, p.x + (long long)r * p.ldx + min(cg * NT * 16 + (lane % (NT * 16)), p.N - 1));
+  constexpr int N_W = NT * KTS + 1;  // loads younger than the cached keys (weights + residual)
+  constexpr int N_KV = 2 * IC * RQ;
+  if (pk.stop == 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence(xres_u); reg_fence(kq[0][0]); reg_fence(wv[0][0]);
+    if ((kq[0][0][0] ^ wv[0][0][0]) == 0x9E3779B9u && xres_u == 7u) p.x[0] = 0.f;
     return;
   }
 
   // 2. q/k RMSNorm + RoPE, v passthrough for the Hq + 2 Hkv vectors of row r: one vector per lane group (LPK lanes
   // x 8 elements), DPP row reductions, rotate-half partner by a DPP row rotation
   {
-    const int e0 = sub * 8, ec = e0 % half;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_KV + N_W) : "memory");
+    reg_fence(xq[0]); reg_fence(xq[1]); reg_fence(qwr[0]); reg_fence(qwr[1]); reg_fence(kwr[0]); reg_fence(kwr[1]);
+    reg_fence(cvr[0]); reg_fence(cvr[1]); reg_fence(svr[0]); reg_fence(svr[1]);
     const bool lo = e0 < half;
-    const int pos = CPOS ? p.const_pos : p.rope_pos[r];
-    float qw[8], kw[8], cv[8], sv[8];
+    float qw[8], kw[8], cv[8], sv[8], xv[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { qw[i] = 1.f; kw[i] = 1.f; }
-    if (p.q_norm) load8f(p.q_norm + e0, qw);
-    if (p.k_norm) load8f(p.k_norm + e0, kw);
-    load8f(p.cos_tab + (long long)pos * half + ec, cv);
-    load8f(p.sin_tab + (long long)pos * half + ec, sv);
-    const int nvec = nq + 2 * nk;
-    for (int t0 = 0; t0 < nvec; t0 += NW * GPW) {
-      const int hh = t0 + w * GPW + grp;
-      const bool ok = hh < nvec;
-      float xv[8];
-      load8f(p.qkv + (long long)r * nvec * D + (long long)(ok ? hh : 0) * D + e0, xv);
-      if (hh < nq + nk) {
-        const bool isq = hh < nq;
-        float ss = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      qw[i] = __uint_as_float(qwr[0][i]); qw[i + 4] = __uint_as_float(qwr[1][i]);
+      kw[i] = __uint_as_float(kwr[0][i]); kw[i + 4] = __uint_as_float(kwr[1][i]);
+      cv[i] = __uint_as_float(cvr[0][i]); cv[i + 4] = __uint_as_float(cvr[1][i]);
+      sv[i] = __uint_as_float(svr[0][i]); sv[i + 4] = __uint_as_float(svr[1][i]);
+      xv[i] = __uint_as_float(xq[0][i]); xv[i + 4] = __uint_as_float(xq[1][i]);
+    }
+    const bool ok = hh < nvec;
+    if (hh < nq + nk) {
+      const bool isq = hh < nq;
+      float ss = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) ss += xv[i] * xv[i];
-        ss = group_sum_dpp<LPK>(ss);
-        const float rs = rsqrtf(ss / (float)D + p.eps);
-        if (isq ? p.q_norm != nullptr : p.k_norm != nullptr) {
+      for (int i = 0; i < 8; ++i) ss += xv[i] * xv[i];
+      ss = group_sum_dpp<LPK>(ss);
+      const float rs = rsqrtf(ss / (float)D + p.eps);
+      if (isq ? p.q_norm != nullptr : p.k_norm != nullptr) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) xv[i] = (isq ? qw[i] : kw[i]) * (xv[i] * rs);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {  // q*cos + rotate_half(q)*sin
-          const float pt = half_partner<LPK>(xv[i]);
-          xv[i] = lo ? xv[i] * cv[i] - pt * sv[i] : xv[i] * cv[i] + pt * sv[i];
-        }
+        for (int i = 0; i < 8; ++i) xv[i] = (isq ? qw[i] : kw[i]) * (xv[i] * rs);
       }
-      if (!ok) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // q*cos + rotate_half(q)*sin
+        const float pt = half_partner<LPK>(xv[i]);
+        xv[i] = lo ? xv[i] * cv[i] - pt * sv[i] : xv[i] * cv[i] + pt * sv[i];
+      }
+    }
+    if (ok) {
       if (hh < nq) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) qs[hh][e0 + i] = xv[i];
       } else {  // as the cache holds them (kv dtype rounding)
         const bool isk = hh < nq + nk;
         const int h = isk ? hh - nq : hh - nq - nk;
-        KV kq[8];
+        KV kv8[8];
         float* dst = isk ? kn[h] : vn[h];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { kq[i] = from_f<KV>(xv[i]); dst[e0 + i] = to_f(kq[i]); }
+        for (int i = 0; i < 8; ++i) { kv8[i] = from_f<KV>(xv[i]); dst[e0 + i] = to_f(kv8[i]); }
         if (cg == 0) {
           KV* cache = (KV*)(isk ? p.k_cache : p.v_cache) + (((long long)r * nk + h) * p.Lmax + kvpos) * D + e0;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) cache[i] = kq[i];
+          for (int i = 0; i < 8; ++i) cache[i] = kv8[i];
         }
       }
     }
   }
   __syncthreads();
   if (pk.stop == 2) {
-    if (qs[0][lane] == 1234.5f && kr[0][0] == 7u) p.x[0] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    reg_fence(kq[0][0]); reg_fence(wv[0][0]);
+    if (qs[0][lane] == 1234.5f && kq[0][0][0] == 7u && wv[0][0][0] == 7u) p.x[0] = 0.f;
     return;
   }
+  // the first batch of cached keys has landed (the cache stores of phase 2, if any, are younger: they only make
+  // this count wait for a few weight fragments too)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_W) : "memory");
+#pragma unroll
+  for (int c = 0; c < IC; ++c)
+#pragma unroll
+    for (int q4 = 0; q4 < RQ; ++q4) { reg_fence(kq[c][q4]); reg_fence(vq[c][q4]); }
+  auto load_batch = [&](int j0) {  // later batches (> GPW * IC cached keys): compiler-tracked loads
+#pragma unroll
+    for (int c = 0; c < IC; ++c)
+#pragma unroll
+      for (int q4 = 0; q4 < RQ; ++q4) {
+        kq[c][q4] = *((const u32x4_t*)kv_addr(j0, c, false) + q4);
+        vq[c][q4] = *((const u32x4_t*)kv_addr(j0, c, true) + q4);
+      }
+  };
 
   // 3. attention of head w: lane group grp owns cached keys grp, grp + GPW, ...; the new key is folded into lane
   // group 0's state; groups merge through a common max + plain sums (VALU permlane butterflies)
@@ -770,12 +802,12 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
         if constexpr (sizeof(KV) == 2) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            kf[2 * i] = __uint_as_float(kr[c][i] << 16); kf[2 * i + 1] = __uint_as_float(kr[c][i] & 0xFFFF0000u);
-            vf[c][2 * i] = __uint_as_float(vr[c][i] << 16); vf[c][2 * i + 1] = __uint_as_float(vr[c][i] & 0xFFFF0000u);
+            kf[2 * i] = __uint_as_float(kq[c][0][i] << 16); kf[2 * i + 1] = __uint_as_float(kq[c][0][i] & 0xFFFF0000u);
+            vf[c][2 * i] = __uint_as_float(vq[c][0][i] << 16); vf[c][2 * i + 1] = __uint_as_float(vq[c][0][i] & 0xFFFF0000u);
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) { kf[i] = __uint_as_float(kr[c][i]); vf[c][i] = __uint_as_float(vr[c][i]); }
+          for (int i = 0; i < 8; ++i) { kf[i] = __uint_as_float(kq[c][i >> 2][i & 3]); vf[c][i] = __uint_as_float(vq[c][i >> 2][i & 3]); }
         }
         if (jj >= nc) {  // masked key: weight exactly 0, keep 0 * v finite
 #pragma unroll
@@ -837,11 +869,19 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
   }
   __syncthreads();
   if (pk.stop == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (to_f(att[w][lane]) == 1234.5f) p.x[0] = 0.f;
     return;
   }
 
   // 4. this head's partial o-proj product (row r = MFMA row 0; rows 1..15 are zero)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int kt = 0; kt < KTS; ++kt) reg_fence(wv[t][kt]);
+  reg_fence(xres_u);
+  const float xres = __uint_as_float(xres_u);
   if (head) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -885,6 +925,7 @@ int attn_oproj_go(const qt_attn_oproj_args& a, hipStream_t s) {
     return QT_ERR_SHAPE;
   } else {
     static const int stop = [] { const char* e = getenv("QT_AO_STOP"); return e ? atoi(e) : 0; }();
+    if (a.Hq + 2 * a.Hkv > 8 * (64 / (D / 8))) return QT_ERR_SHAPE;  // one q/k/v vector per lane group
     const int cgs = ((a.N + 15) / 16 + NT - 1) / NT;
     hipLaunchKernelGGL((attn_oproj_k<WT, WT, D, NREP, NT, CPOS>), dim3(cgs * a.R), dim3(512), 0, s, AOK{a, stop});
     return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;

@@ -101,6 +101,18 @@ QT_DEV float wave_sum_dpp(float v) {
          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
 }
 
+// Untracked loads: hipcc inserts no waits for inline-asm loads, so a kernel can keep them in flight across its own
+// loops and phases.  The caller waits with an explicit `s_waitcnt vmcnt(n)` (n = its loads issued after this one)
+// and then reg_fence()s every destination before the first use, so nothing reads the register before the data lands.
+QT_DEV void asm_ld16(u32x4_t& r, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+QT_DEV void asm_ld4(unsigned& r, const void* p) {
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+template <typename T>
+QT_DEV void reg_fence(T& x) { asm volatile("" : "+v"(x)); }
+
 QT_DEV float silu_f(float g) { return g / (1.0f + expf(-g)); }
 QT_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 QT_DEV float elu_f(float x) { return x > 0.f ? x : expm1f(x); }

@@ -445,14 +445,30 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     if (tid == 0) p.tok_out[r] = tok;
     return;
   }
-  if (p.emb_table) {  // next-step input row: the chosen token's (projected) embedding
+  if (p.emb_table) {  // next-step input row: the chosen token's (projected) embedding (+ its layer-0 q/k/v row)
     const float* src = p.emb_table + (long long)tok * p.emb_dim;
     float* dst = p.emb_out + (long long)r * p.emb_ld;
     bf16_t* d16 = p.emb_out16 ? (bf16_t*)p.emb_out16 + (long long)r * p.emb_ld16 : nullptr;
-    for (int i = tid * 4; i < p.emb_dim; i += NT * 4) {
-      const f32x4_t v = *(const f32x4_t*)(src + i);
-      *(f32x4_t*)(dst + i) = v;
-      if (d16) *(uint2*)(d16 + i) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    const float* src2 = p.emb2_table ? p.emb2_table + (long long)tok * p.emb2_dim : nullptr;
+    float* dst2 = p.emb2_table ? p.emb2_out + (long long)r * p.emb2_ld : nullptr;
+    constexpr int G2 = 4;  // second-table float4s per thread per pass, all loads of a pass issued before its stores
+    for (int i = tid * 4, i2 = tid * 4; i < p.emb_dim || (src2 && i2 < p.emb2_dim); i += NT * 4, i2 += NT * 4 * G2) {
+      f32x4_t v = {0.f, 0.f, 0.f, 0.f}, v2[G2];
+      if (i < p.emb_dim) v = *(const f32x4_t*)(src + i);
+      if (src2) {
+#pragma unroll
+        for (int j = 0; j < G2; ++j)
+          if (i2 + j * NT * 4 < p.emb2_dim) v2[j] = *(const f32x4_t*)(src2 + i2 + j * NT * 4);
+      }
+      if (i < p.emb_dim) {
+        *(f32x4_t*)(dst + i) = v;
+        if (d16) *(uint2*)(d16 + i) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      }
+      if (src2) {
+#pragma unroll
+        for (int j = 0; j < G2; ++j)
+          if (i2 + j * NT * 4 < p.emb2_dim) *(f32x4_t*)(dst2 + i2 + j * NT * 4) = v2[j];
+      }
     }
   }
   if (tid != 0) return;
@@ -472,6 +488,7 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
   if (a->emb_out16 && (!a->emb_table || a->emb_ld16 % 4)) return QT_ERR_SHAPE;
+  if (a->emb2_table && (!a->emb_table || !a->emb2_out || a->emb2_dim % 4 || a->emb2_ld % 4)) return QT_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
   const SK k{*a, stop};

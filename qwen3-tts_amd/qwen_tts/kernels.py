@@ -258,9 +258,9 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
-           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None):
+           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None):
     """emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
-    emb16 = (out bf16 rows, ld): its bf16 copy.
+    emb16 = (out bf16 rows, ld): its bf16 copy; emb2 = (table2 fp32 [V][D2], out2 fp32 rows, ld2): a second row.
     seed_ptr: device int64 [1] read at run time instead of `seed` (graph-captured samplers)."""
     a = _hip.SampleArgs()
     a.logits, a.R, a.V, a.ld = ptr(logits), R, V, ld
@@ -277,6 +277,8 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
         a.emb_table, a.emb_dim, a.emb_out, a.emb_ld = ptr(emb[0]), emb[0].shape[1], ptr(emb[1]), emb[2]
         if emb16 is not None:
             a.emb_out16, a.emb_ld16 = ptr(emb16[0]), emb16[1]
+        if emb2 is not None:
+            a.emb2_table, a.emb2_dim, a.emb2_out, a.emb2_ld = ptr(emb2[0]), emb2[0].shape[1], ptr(emb2[1]), emb2[2]
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 

@@ -63,13 +63,14 @@ class _Stack:
         if self.cos.shape[0] < npos:
             self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
 
-    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None):
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None, qkv0=False):
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
         decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention.
         x16 (bf16 mode, R <= 16): bf16 shadow of x, kept current by every writer of x (the residual-add epilogues
         store both) and read as the A operand of the RMS-normalised GEMVs (QKV, gate/up): their MFMA rounds A to
         bf16 anyway, so only the RMS row sums change (they come from the bf16 values, as the reference's bf16
-        residual stream gives them) while the activation fetch halves."""
+        residual stream gives them) while the activation fetch halves.
+        qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler)."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
         if x16 is not None and ("mlp_ws" in scratch or R > 16):
@@ -77,7 +78,8 @@ class _Stack:
         xa = x if x16 is None else x16
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
+            if not (qkv0 and li == 0):
+                K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                     self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"], x16=x16)
@@ -111,6 +113,8 @@ FUSED_MLP = os.environ.get("QT_FUSED_MLP", "0") == "1"
 ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
+# code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
+QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -280,6 +284,18 @@ class TalkerEngine:
         Hc = cc["hidden_size"]
         self.cp_in_tabs = [self._proj_table(self.ecp[g], Hc) for g in range(self.G - 2)]
         self.cp_in_tab0 = self._proj_table(self.emb0, Hc)
+        # bf16 mode: the code predictor's layer-0 q/k/v projection of every decode-step input row, precomputed per
+        # table ([V][qkv_w] fp32, from the bf16-rounded rows as the x16 shadow feeds the decode GEMV): the sampler that
+        # picks a step's token also gathers its q/k/v row, so decode steps skip the layer-0 QKV GEMV (14 launches/frame)
+        self.cp_qkv_tabs = None
+        if self.wdt == torch.bfloat16 and QKV0_TAB:
+            L0, c = self.cp.layers[0], self.cp
+            self.cp_qkv_tabs = []
+            for tab in self.cp_in_tabs:
+                t16 = tab.to(torch.bfloat16)
+                out = torch.empty(tab.shape[0], c.qkv_w, dtype=torch.float32, device=dev)
+                K.gemm(t16, L0.qkv, out, tab.shape[0], Hc, c.qkv_w, rms=True, eps=c.eps)
+                self.cp_qkv_tabs.append(out)
         self._sessions: Dict[tuple, List[Session]] = {}
         self._streams: List[torch.cuda.Stream] = []
         # decode row groups: the batch is split into this many independent groups, each with its own session,
@@ -431,7 +447,8 @@ class TalkerEngine:
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
             x16 = None if ln.x16 is None else ln.x16[:nb]
-            c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16)
+            c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16,
+                      qkv0=self.cp_qkv_tabs is not None)
             self._cp_head(s, ln, x, Hc, g, x16)
 
     def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None):
@@ -442,7 +459,9 @@ class TalkerEngine:
                  seed_ptr=s.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
                  codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base + ln.b0,
                  emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None,
-                 emb16=(ln.x16, c.H) if ln.x16 is not None and g < self.G - 2 else None)
+                 emb16=(ln.x16, c.H) if ln.x16 is not None and g < self.G - 2 else None,
+                 emb2=(self.cp_qkv_tabs[g], ln.sc["qkv"], c.qkv_w) if self.cp_qkv_tabs is not None and g < self.G - 2
+                 else None)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,

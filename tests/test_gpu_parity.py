@@ -469,6 +469,29 @@ def test_sample_greedy_processors():
         assert tok.cpu().long().tolist() == ref.tolist()
 
 
+def test_sample_next_step_rows():
+    """The sampler's next-step outputs: the chosen token's table row (fp32), its bf16 copy (the residual shadow)
+    and the second table's row (the code predictor's precomputed layer-0 q/k/v), each at its own row stride."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(3)
+    R, V, D, D2 = 8, 2048, 1024, 4096
+    logits = torch.randn(R, V, generator=g).to(dev)
+    tab = torch.randn(V, D, generator=g).to(dev)
+    tab2 = torch.randn(V, D2, generator=g).to(dev)
+    out = torch.zeros(R, D + 8, device=dev)
+    out16 = torch.zeros(R, D + 16, dtype=torch.bfloat16, device=dev)
+    out2 = torch.zeros(R, D2 + 4, device=dev)
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(logits, R, V, V, tok, emb=(tab, out, D + 8), emb16=(out16, D + 16), emb2=(tab2, out2, D2 + 4))
+    t = tok.long()
+    assert torch.equal(t, logits.argmax(-1))
+    torch.testing.assert_close(out[:, :D], tab[t], atol=0, rtol=0)
+    torch.testing.assert_close(out16[:, :D], tab[t].to(torch.bfloat16), atol=0, rtol=0)
+    torch.testing.assert_close(out2[:, :D2], tab2[t], atol=0, rtol=0)
+    assert not out[:, D:].any() and not out16[:, D:].float().any() and not out2[:, D2:].any()
+
+
 def test_sample_distribution_topk():
     """Sampling parity is distribution-level (RNG streams differ by device): frequencies vs probabilities."""
     from qwen_tts import kernels as Kn
@@ -891,6 +914,36 @@ def test_talker_bf16_runs_and_tracks_fp32(tiny_models):
     c16, _ = _run_case(m16, "cv_b1_nonstream", case, 0, cfg)
     assert c16[0].shape == c32[0].shape
     assert (c16[0][:2, 0] == c32[0][:2, 0]).all()  # the first tokens agree; later frames may drift in bf16
+
+
+def test_bf16_decode_shortcuts_track_the_plain_path(tiny_models, monkeypatch):
+    """bf16 decode shortcuts -- the bf16 residual shadow read by the RMS-normalised GEMVs (talker.X16) and the code
+    predictor's layer-0 q/k/v gathered from precomputed tables (talker.QKV0_TAB) -- change only roundings (RMS sums
+    from the bf16-rounded activations the MFMA reads anyway; another GEMM's summation order for the tables): greedy
+    codes and per-frame hidden states stay with the plain bf16 path."""
+    from cases import talker_cases
+    from qwen_tts import talker as T
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    case = talker_cases()["cv_b2_stream_dialect"]
+    idx = list(talker_cases()).index("cv_b2_stream_dialect")
+    runs = {}
+    for x16, tab in ((False, False), (True, False), (True, True)):
+        monkeypatch.setattr(T, "X16", x16)
+        monkeypatch.setattr(T, "QKV0_TAB", tab)
+        m = TTSModel(cfg, W, dtype="bf16")
+        assert (m.engine.cp_qkv_tabs is not None) == tab
+        runs[(x16, tab)] = _run_case(m, "cv_b2_stream_dialect", case, idx, cfg)
+    c0, h0 = runs[(False, False)]
+    for key in ((True, False), (True, True)):
+        c, h = runs[key]
+        for a, b, ha, hb in zip(c, c0, h, h0):
+            n = min(a.shape[0], b.shape[0])
+            assert n >= 4
+            assert torch.equal(a[:4], b[:4]), key  # greedy codes of the first frames agree exactly
+            assert (a[:n] == b[:n]).float().mean() >= 0.9, key
+            rel = (ha[:4] - hb[:4]).norm() / hb[:4].norm()
+            assert rel < 3e-2, (key, float(rel))
 
 
 # ------------------------------------------------------------------------------------------ codec
