@@ -23,7 +23,7 @@ def main():
     for name, N, Kk, rms, epi in shapes:
         nmat = max(2, int(600e6 // (N * Kk * 2)))
         Ws = [K.tile_linear(torch.randn(N, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
-        A = torch.randn(8, Kk, device=dev)
+        A = torch.randn(8, Kk, device=dev).to(torch.bfloat16)  # production A: x16 shadow / att / SwiGLU out (bf16)
         out = torch.zeros(8, N, device=dev)
         ep = [_hip.EPI_STORE, _hip.EPI_ADD, _hip.EPI_SWIGLU][epi]
         o = out if ep != _hip.EPI_SWIGLU else torch.zeros(8, N // 2, device=dev, dtype=torch.bfloat16)
