@@ -221,6 +221,8 @@ typedef struct qt_sample_args {
   /* optional second gathered row (with emb_table): emb2_out[r*emb2_ld + i] = emb2_table[tok*emb2_dim + i] -- the
    * code predictor's layer-0 q/k/v projection of every table row, precomputed, so the next step skips that GEMV */
   const float* emb2_table; int emb2_dim; float* emb2_out; long long emb2_ld;
+  int algo;  /* top-k (<= 64) sampling path, tests / measurement: 0 auto (histogram, per-wave on fall-through),
+              * 1 per-wave candidate lists only, 2 histogram (same as 0).  Same Philox draws, same tokens. */
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 

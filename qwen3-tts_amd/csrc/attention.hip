@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
   const int nsplit = gridDim.z, z = blockIdx.z;
   const int per_split = (n + nsplit - 1) / nsplit;
   const int j_lo = min(n, z * per_split), j_hi = min(n, j_lo + per_split);
-  if (j_lo + gid < j_hi) load_chunk(j_lo + gid);  // in flight while phase 0 runs
+  load_chunk(j_lo + gid);  // in flight while phase 0 runs (clamped addresses: no branch around the loads)
   // ---- phase 0: norm + rope of q heads / new k, v passthrough; append to cache
   if (w < NREP + 2) {
     const int hh = w < NREP ? h * NREP + w : (w == NREP ? nq + h : nq + nk + h);
@@ -432,11 +432,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
     }
   };
   constexpr int GIC = G * IC;
+  // The prefetches are unconditional (clamped addresses): a branch around them made hipcc's merged wait counts
+  // drain the prefetch before the current chunk was consumed, serialising the two round trips.
   for (int j0 = j_lo + gid; j0 < j_hi; j0 += 2 * GIC) {
-    if (j0 + GIC < j_hi) load_into(j0 + GIC, kn, vn);
+    load_into(j0 + GIC, kn, vn);
     consume(kr, vr, j0);
     if (j0 + GIC >= j_hi) break;
-    if (j0 + 2 * GIC < j_hi) load_into(j0 + 2 * GIC, kr, vr);
+    load_into(j0 + 2 * GIC, kr, vr);
     consume(kn, vn, j0 + GIC);
   }
   // merge lane groups inside the wave (ds_bpermute butterflies: the permlane transpose-reduce GroupMerge was

@@ -35,20 +35,22 @@ __global__ void gather_rows_k(const T* __restrict__ tab, const int* __restrict__
 }
 
 template <typename ET>
-__global__ __launch_bounds__(256) void frame_embed_k(const ET* __restrict__ e0, const ET* __restrict__ ecp, int V0,
+__global__ __launch_bounds__(64) void frame_embed_k(const ET* __restrict__ e0, const ET* __restrict__ ecp, int V0,
                                                      int Vcp, int G, int H, const int* __restrict__ codes,
                                                      long long codes_ld, const int* __restrict__ step,
                                                      const float* __restrict__ trailing, int T,
                                                      const float* __restrict__ pad, float* __restrict__ x,
                                                      bf16_t* __restrict__ x16) {
-  // ET: table dtype.  Codes to LDS once, then every thread issues its 16 row-slice loads before summing.
+  // ET: table dtype.  Block (b, y) sums dims [y * 8 * blockDim, ...) of row b (several blocks per row: the 16
+  // table-row slices are spread over CUs instead of one CU taking in the whole 16-row gather).  Codes to LDS once,
+  // then every thread issues its 16 row-slice loads before summing.
   __shared__ int cs[32];
   const int b = blockIdx.x;
   const int t = *step;
   if (threadIdx.x < G) cs[threadIdx.x] = codes[(long long)b * codes_ld + (long long)t * G + threadIdx.x];
   __syncthreads();
   const float* tr = t < T ? trailing + ((long long)b * T + t) * H : pad;
-  for (int i = threadIdx.x * 8; i < H; i += blockDim.x * 8) {
+  for (int i = (blockIdx.y * blockDim.x + threadIdx.x) * 8; i < H; i += gridDim.y * blockDim.x * 8) {
     float acc[8], v[8];
     load8f(e0 + (long long)cs[0] * H + i, acc);
     for (int g = 1; g < G; ++g) {  // sum order: cat([...16 codebooks]).sum(1) then + text (M:1681-1692)
@@ -182,11 +184,12 @@ extern "C" int qt_frame_embed(const void* e0, const void* ecp, int dtype, int V0
                               const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
                               const float* pad, float* x, void* x16, int B, void* s) {
   if (B <= 0 || H <= 0 || G < 1 || G > 32 || H % 8) return QT_ERR_SHAPE;
+  const dim3 grid(B, (H + 511) / 512);  // one wave per 512 dims
   if (dtype == QT_BF16)
-    hipLaunchKernelGGL(frame_embed_k<bf16_t>, dim3(B), dim3(256), 0, (hipStream_t)s, (const bf16_t*)e0,
+    hipLaunchKernelGGL(frame_embed_k<bf16_t>, grid, dim3(64), 0, (hipStream_t)s, (const bf16_t*)e0,
                        (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
   else if (dtype == QT_F32)
-    hipLaunchKernelGGL(frame_embed_k<float>, dim3(B), dim3(256), 0, (hipStream_t)s, (const float*)e0,
+    hipLaunchKernelGGL(frame_embed_k<float>, grid, dim3(64), 0, (hipStream_t)s, (const float*)e0,
                        (const float*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
   else
     return QT_ERR_DTYPE;

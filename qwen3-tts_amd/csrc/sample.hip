@@ -107,6 +107,10 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   __shared__ __attribute__((aligned(16))) int gi_s[16];
   __shared__ __attribute__((aligned(16))) float gb_s[16];
   __shared__ unsigned tk_s;
+  __shared__ int hist_s[NT];  // value histogram of the histogram fast path (one bin per thread)
+  __shared__ float hl_s[2][64];
+  __shared__ int hli_s[2][64], hln_s[2], hb_s[2], htok_s;
+  __shared__ float wmx_s[4];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = p.V;
   const float* lg = p.logits + (long long)r * p.ld;
@@ -185,7 +189,107 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     // step, substep, row, token) -- an exact sample of softmax(s / T) restricted to the top-k set.  A wave left
     // with > 64 tied keys falls back to the block search.
     bool fast = false;
-    if (p.top_k > 0 && p.top_k < V && p.top_k <= 64 && p.top_p >= 1.0f) {
+    const bool fast_ok = p.top_k > 0 && p.top_k < V && p.top_k <= 64 && p.top_p >= 1.0f;
+    // Histogram fast path (k <= 64, no top-p; p.algo 0 or 2): the k-th largest score located by a 256-bin value
+    // histogram below the row maximum (bin = floor((max - s) * HB), HB bins per unit of s / T), then resolved exactly
+    // among the boundary bin's scores; kept = {s >= k-th largest} (ties kept, TopKLogitsWarper).  Wave 0 then draws
+    // the Gumbel-max over the kept set with the per-wave path's Philox stream (same token for the same kept set).
+    // Falls through to the per-wave path when the top k span more than 256 / HB below the max or the boundary bin
+    // holds more than 64 scores.  5 block barriers in all.
+    if (fast_ok && p.algo != 1) {
+      constexpr float HB = 16.f;
+      hist_s[tid] = 0;
+      const float wm = wave_max(mx);
+      if (lane == 0) wmx_s[w] = wm;
+      if (tid < 2) hln_s[tid] = 0;
+      __syncthreads();
+      const float M = fmaxf(fmaxf(wmx_s[0], wmx_s[1]), fmaxf(wmx_s[2], wmx_s[3]));
+      int bin[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const float d = (M - s[j]) * HB;  // >= 0; -inf scores give +inf
+        bin[j] = (tid + j * NT < V && d < (float)NT) ? (int)d : NT;
+        if (bin[j] < NT) atomicAdd(&hist_s[bin[j]], 1);
+      }
+      __syncthreads();
+      if (w == 0) {  // first bin (from the top) where the running count reaches k: scan of 4 bins per lane
+        int h[4], loc = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { h[i] = hist_s[lane * 4 + i]; loc += h[i]; }
+        int scan = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(scan, o, 64);
+          if (lane >= o) scan += y;
+        }
+        const int excl = scan - loc;
+        const bool cross = excl < p.top_k && scan >= p.top_k;
+        if (cross) {
+          int c = excl, b = -1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (b < 0) {
+              if (c + h[i] >= p.top_k) b = lane * 4 + i;
+              else c += h[i];
+            }
+          }
+          hb_s[0] = b; hb_s[1] = c;  // boundary bin, scores strictly above it
+        }
+        if (lane == 63 && scan < p.top_k) hb_s[0] = -1;  // the top k reach below the histogram: fall through
+      }
+      __syncthreads();
+      const int bs = hb_s[0];
+      if (bs >= 0) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {  // list 0: scores above the boundary bin (all kept); list 1: the bin's scores
+          if (bin[j] <= bs) {
+            const int l = bin[j] < bs ? 0 : 1;
+            const int pos = atomicAdd(&hln_s[l], 1);
+            if (pos < 64) { hl_s[l][pos] = s[j]; hli_s[l][pos] = tid + j * NT; }
+          }
+        }
+      }
+      __syncthreads();
+      if (bs >= 0 && hln_s[1] <= 64) {
+        fast = true;
+        if (w == 0) {
+          const int n0 = hln_s[0], n1 = hln_s[1], need = p.top_k - hb_s[1];  // 1 <= need <= n1
+          const float mine = lane < n1 ? hl_s[1][lane] : -INFINITY;
+          int gt = 0, ge = 0;
+          for (int i = 0; i < n1; ++i) {
+            const float o = hl_s[1][i];
+            gt += o > mine ? 1 : 0;
+            ge += o >= mine ? 1 : 0;
+          }
+          // v_k: the need-th largest boundary score (every lane whose rank window covers `need` holds that value)
+          const unsigned long long kb = __ballot(lane < n1 && gt < need && need <= ge);
+          const float vk = __shfl(mine, kb ? __ffsll((long long)kb) - 1 : 0, 64);
+          float best = -INFINITY;
+          int bi = 0x7fffffff;
+          auto draw = [&](float sc, int ti) {
+            const float u = philox_uniform4(seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)ti);
+            const float g = okey_inv(okey(sc)) - __logf(-__logf(u));
+            if (g > best || (g == best && ti < bi)) { best = g; bi = ti; }
+          };
+          if (lane < n0) draw(hl_s[0][lane], hli_s[0][lane]);
+          if (lane < n1 && mine >= vk) draw(mine, hli_s[1][lane]);
+          argmax_dpp<0xB1>(best, bi);
+          argmax_dpp<0x4E>(best, bi);
+          argmax_dpp<0x141>(best, bi);
+          argmax_dpp<0x140>(best, bi);
+#pragma unroll
+          for (int rr = 16; rr < 64; rr += 16) {
+            const float ob = __shfl(best, rr, 64);
+            const int oi = __shfl(bi, rr, 64);
+            if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+          }
+          if (lane == 0) htok_s = bi == 0x7fffffff ? 0 : bi;
+        }
+        __syncthreads();
+        tok = htok_s;
+      }
+    }
+    if (fast_ok && !fast) {
       int nv = 0;
 #pragma unroll
       for (int j = 0; j < PER; ++j) nv += key[j] != 0u;
@@ -449,22 +553,23 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     const float* src = p.emb_table + (long long)tok * p.emb_dim;
     float* dst = p.emb_out + (long long)r * p.emb_ld;
     bf16_t* d16 = p.emb_out16 ? (bf16_t*)p.emb_out16 + (long long)r * p.emb_ld16 : nullptr;
-    const float* src2 = p.emb2_table ? p.emb2_table + (long long)tok * p.emb2_dim : nullptr;
-    float* dst2 = p.emb2_table ? p.emb2_out + (long long)r * p.emb2_ld : nullptr;
-    constexpr int G2 = 4;  // second-table float4s per thread per pass, all loads of a pass issued before its stores
-    for (int i = tid * 4, i2 = tid * 4; i < p.emb_dim || (src2 && i2 < p.emb2_dim); i += NT * 4, i2 += NT * 4 * G2) {
-      f32x4_t v = {0.f, 0.f, 0.f, 0.f}, v2[G2];
-      if (i < p.emb_dim) v = *(const f32x4_t*)(src + i);
-      if (src2) {
+    // every load of a pass is issued before its stores, at clamped addresses (a branch around a load makes hipcc
+    // wait for it right away); without a second table its loads re-read the first table's row
+    const bool two = p.emb2_table != nullptr;
+    const float* src2 = two ? p.emb2_table + (long long)tok * p.emb2_dim : src;
+    const int lim2 = (two ? p.emb2_dim : p.emb_dim) - 4;
+    float* dst2 = two ? p.emb2_out + (long long)r * p.emb2_ld : nullptr;
+    constexpr int G2 = 4;  // second-table float4s per thread per pass
+    for (int i = tid * 4, i2 = tid * 4; i < p.emb_dim || (two && i2 < p.emb2_dim); i += NT * 4, i2 += NT * 4 * G2) {
+      f32x4_t v2[G2];
+      const f32x4_t v = *(const f32x4_t*)(src + min(i, p.emb_dim - 4));
 #pragma unroll
-        for (int j = 0; j < G2; ++j)
-          if (i2 + j * NT * 4 < p.emb2_dim) v2[j] = *(const f32x4_t*)(src2 + i2 + j * NT * 4);
-      }
+      for (int j = 0; j < G2; ++j) v2[j] = *(const f32x4_t*)(src2 + min(i2 + j * NT * 4, lim2));
       if (i < p.emb_dim) {
         *(f32x4_t*)(dst + i) = v;
         if (d16) *(uint2*)(d16 + i) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
       }
-      if (src2) {
+      if (two) {
 #pragma unroll
         for (int j = 0; j < G2; ++j)
           if (i2 + j * NT * 4 < p.emb2_dim) *(f32x4_t*)(dst2 + i2 + j * NT * 4) = v2[j];

@@ -79,7 +79,8 @@ class SampleArgs(ctypes.Structure):
                 ("codes_col", c_int), ("codes_step_off", c_int), ("row_base", c_int),
                 ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll),
                 ("seed_ptr", c_void_p), ("debug_u", c_float), ("emb_out16", c_void_p), ("emb_ld16", c_ll),
-                ("emb2_table", c_void_p), ("emb2_dim", c_int), ("emb2_out", c_void_p), ("emb2_ld", c_ll)]
+                ("emb2_table", c_void_p), ("emb2_dim", c_int), ("emb2_out", c_void_p), ("emb2_ld", c_ll),
+                ("algo", c_int)]
 
 
 class MlpArgs(ctypes.Structure):

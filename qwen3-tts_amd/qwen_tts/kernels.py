@@ -258,7 +258,7 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
-           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None):
+           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None, algo=0):
     """emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
     emb16 = (out bf16 rows, ld): its bf16 copy; emb2 = (table2 fp32 [V][D2], out2 fp32 rows, ld2): a second row.
     seed_ptr: device int64 [1] read at run time instead of `seed` (graph-captured samplers)."""
@@ -272,7 +272,7 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     a.seed, a.step, a.substep, a.tok_out = seed & (2 ** 64 - 1), ptr(step), substep, ptr(tok_out)
     a.codes, a.codes_ld, a.codes_w, a.codes_col, a.codes_step_off = ptr(codes), codes_ld, codes_w, codes_col, codes_step_off
     a.row_base = row_base
-    a.seed_ptr, a.debug_u = ptr(seed_ptr), float(debug_u)
+    a.seed_ptr, a.debug_u, a.algo = ptr(seed_ptr), float(debug_u), int(algo)
     if emb is not None:
         a.emb_table, a.emb_dim, a.emb_out, a.emb_ld = ptr(emb[0]), emb[0].shape[1], ptr(emb[1]), emb[2]
         if emb16 is not None:

@@ -469,6 +469,36 @@ def test_sample_greedy_processors():
         assert tok.cpu().long().tolist() == ref.tolist()
 
 
+@pytest.mark.parametrize("V,scale,ties", [(2048, 0.7, False), (2048, 3.0, False), (3072, 1.0, True), (2048, 40.0, False),
+                                          (2048, 0.02, False)])
+def test_sample_histogram_topk_matches_per_wave_path(V, scale, ties):
+    """The histogram top-k path (default) and the per-wave candidate path (algo=1) keep the same top-k set and draw
+    the same Philox-keyed Gumbel-max token, for spreads inside the histogram (0.7, 3 units), beyond it (40: falls
+    through) and flat rows (0.02: the boundary bin overflows, falls through).  With many ties (scores on a 0.25 grid)
+    the per-wave path can overflow its candidate lists and draw by inverse CDF instead (another use of the Philox
+    stream), so there both paths are only checked to draw from the kept set (every score >= the k-th largest)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    g = torch.Generator().manual_seed(11)
+    R = 16
+    logits = torch.randn(R, V, generator=g) * scale
+    if ties:
+        logits = (logits * 4).round() / 4  # many equal scores, also at the k-th
+    lg = logits.to(dev)
+    for k in (1, 20, 50, 64):
+        for seed in range(6):
+            toks = []
+            for algo in (0, 1):
+                tok = torch.zeros(R, dtype=torch.int32, device=dev)
+                Kn.sample(lg, R, V, V, tok, do_sample=True, top_k=k, temperature=0.9, seed=seed, algo=algo)
+                toks.append(tok.cpu())
+            if not ties:
+                assert torch.equal(toks[0], toks[1]), (k, seed)
+            kth = logits.topk(k, -1).values[:, -1:]
+            for t in toks:
+                assert bool((logits.gather(1, t.long()[:, None]) >= kth).all()), (k, seed)
+
+
 def test_sample_next_step_rows():
     """The sampler's next-step outputs: the chosen token's table row (fp32), its bf16 copy (the residual shadow)
     and the second table's row (the code predictor's precomputed layer-0 q/k/v), each at its own row stride."""
