@@ -1,7 +1,7 @@
 # Round measurement set (tag = $1): GPU tests, the default bench line (roofline + CPU baseline), rocprof
 # kernel-trace stats of the same bench command, then two PMC passes (FETCH_SIZE, WRITE_SIZE) on the roofline kernel.
 set -e
-tag=${1:-r01}
+tag=${1:-r02}
 root=$(pwd)
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1
 timeout -k 10 600 python bench.py > gpurun_out/${tag}_bench.log 2>&1
