@@ -767,6 +767,12 @@ void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
   else launch_gemv_u<WT, AT, OT, WPB, 4>(p, nt, s);
 }
 
+// smallest row count routed to the LDS-tiled implicit GEMM (QT_IGEMM_MIN_M overrides, measurement)
+inline int igemm_min_m() {
+  static const int v = [] { const char* e = getenv("QT_IGEMM_MIN_M"); return e ? atoi(e) : 128; }();
+  return v;
+}
+
 template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
@@ -785,7 +791,7 @@ int launch(const GemmP& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_n1_k<AT, WT, OT>), dim3(batches * ((p.t_out + 255) / 256)), dim3(256), smem, s, p);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
-  } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 && p.M >= 128 &&
+  } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 && p.M >= igemm_min_m() &&
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
     const int taps = p.taps == 0 ? 1 : p.taps, dil = p.taps == 0 ? 1 : p.dil;
     const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;

@@ -1,6 +1,6 @@
 """Decode GEMV (M = 8) at the talker / code-predictor shapes with weights cold (cycling through > 600 MB, every
-launch streams HBM) vs hot (one matrix re-read, resident in the 256 MiB Infinity Cache): how much of each launch
-is HBM time and how much is fixed cost."""
+launch streams HBM), Infinity-Cache resident (cycling through ~120 MB: more than the 32 MiB of L2, less than the
+256 MiB Infinity Cache) and hot (one matrix re-read, L2-resident): how much of each launch is memory time."""
 import os
 import sys
 import torch
@@ -35,8 +35,13 @@ def main():
 
         def hot():
             K.gemm(A, Ws[0], o, 8, Kk, N, rms=rms, eps=1e-6, epi=ep, splitk=sk)
+        nm = max(2, int(120e6 // (N * Kk * 2)))  # > the 32 MiB of L2, < the 256 MiB Infinity Cache
+
+        def mall():
+            K.gemm(A, Ws[it["i"] % nm], o, 8, Kk, N, rms=rms, eps=1e-6, epi=ep, splitk=sk)
+            it["i"] += 1
         mb = N * Kk * 2 / 1e6
-        for lab, f in ((("cold", cold),) if only_cold else (("cold", cold), ("hot", hot))):
+        for lab, f in ((("cold", cold),) if only_cold else (("cold", cold), ("mall", mall), ("hot", hot))):
             us = timed(f, f"{name} {N}x{Kk} ({mb:.1f} MB) {lab}")
             print(f"{'':60s} -> {mb * 1e3 / us:8.1f} GB/s", flush=True)
         del Ws

@@ -1,0 +1,36 @@
+"""Talker prefill linears at streaming-text prompt sizes (M = 8 x ~10 rows), 1.7B dims: per-launch time of each
+shape on the path qt_gemm picks (QT_IGEMM_MIN_M moves the implicit-GEMM threshold for A/B)."""
+import os
+import sys
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "qwen3-tts_amd"))
+from qwen_tts import kernels as K, _hip  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from microbench import timed  # noqa: E402
+
+dev = torch.device("cuda:0")
+
+
+def main():
+    shapes = [("qkv", 4096, 2048, True, 0, torch.float32), ("o", 2048, 2048, False, 1, torch.bfloat16),
+              ("gate-up", 12288, 2048, True, 2, torch.float32), ("down", 2048, 6144, False, 1, torch.bfloat16)]
+    for M in (80, 160):
+        for name, N, Kk, rms, epi, adt in shapes:
+            nmat = max(2, int(600e6 // (N * Kk * 2)))
+            Ws = [K.tile_linear(torch.randn(N, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
+            A = torch.randn(M, Kk, device=dev).to(adt)
+            ep = [_hip.EPI_STORE, _hip.EPI_ADD, _hip.EPI_SWIGLU][epi]
+            o = torch.zeros(M, N, device=dev) if ep != _hip.EPI_SWIGLU else torch.zeros(M, N // 2, device=dev,
+                                                                                          dtype=torch.bfloat16)
+            it = {"i": 0}
+
+            def f():
+                K.gemm(A, Ws[it["i"] % nmat], o, M, Kk, o.shape[1] if ep != _hip.EPI_SWIGLU else N, rms=rms,
+                       eps=1e-6, epi=ep)
+                it["i"] += 1
+            timed(f, f"prefill {name} M={M} {N}x{Kk}")
+            del Ws
+
+
+if __name__ == "__main__":
+    main()

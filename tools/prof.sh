@@ -9,5 +9,6 @@ rc=$?
 echo rc=$rc >> gpurun_out/$tag.log
 tr=$(find gpurun_out/$tag -name "*kernel_trace.csv" | head -1)
 [ -n "$tr" ] && python3 tools/trace_summary.py "$tr" gpurun_out/$tag/summary.txt
+[ -n "$tr" ] && python3 tools/trace_position.py "$tr" gpurun_out/$tag/position.txt
 find gpurun_out/$tag -name "*kernel_trace*" -delete
 exit $rc
