@@ -631,7 +631,9 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
   constexpr bool BF = sizeof(WT) == 2;
   constexpr int E = BF ? 8 : 4, KT = 4 * E;
   constexpr int KS = NREP * D, KTS = KS / KT;  // o-proj K slice of one kv head, in k tiles
-  constexpr int LPK = D / 8, GPW = 64 / LPK, IC = 4, RW = sizeof(KV) * 8 / 4;
+  // IC = cached keys per lane group per batch; 2 at NREP 4 (4 spilled asm-loaded registers to scratch before their
+  // data landed -- tools/asm_audit.py)
+  constexpr int LPK = D / 8, GPW = 64 / LPK, IC = NREP >= 4 ? 2 : 4, RW = sizeof(KV) * 8 / 4;
   constexpr int ALD = KS + 4 * (BF ? 2 : 1);  // 16 B pad per row
   typedef typename std::conditional<BF, bf16_t, float>::type AT;
   __shared__ float qs[NW * NREP][D];

@@ -202,6 +202,10 @@ class CodecDecoder:
         K.clamp_pcm(pcm, pcm.numel(), pcm)
         return pcm.view(B, L)
 
+    def stream(self, B: int, max_frames: int) -> "CodecStream":
+        """A stateful incremental decode of up to max_frames frames (one reference chunk with its context)."""
+        return CodecStream(self, B, max_frames)
+
     def chunked_decode(self, codes: torch.Tensor, chunk_size=300, left_context_size=25) -> torch.Tensor:
         """K:885-895 (codes [B, T, 16]; same chunk / left-context semantics, including the >300 quirks)."""
         wavs, start, T = [], 0, codes.shape[1]
@@ -225,3 +229,151 @@ class CodecDecoder:
         wav = self.chunked_decode(audio_codes)
         lengths = (audio_codes[..., 0] > 0).sum(1) * self.ccfg["decode_upsample_rate"]
         return [a[:int(l)] for a, l in zip(wav, lengths)]
+
+
+class CodecStream:
+    """Stateful incremental form of CodecDecoder.forward: frames are fed as they are generated and
+    every output sample is computed once.  After n frames have been fed, samples [0, 1920 n - 555) of
+    forward(all n frames) are available -- the same prefix, since every stage only looks back (causal convs,
+    sliding-window attention) except the decoder blocks' transposed convs, whose output row t needs input rows t and
+    t + 1 (their one-row lookahead is what the 555-sample tail is).  State per stage: the last (taps - 1) x dil input
+    rows of every causal conv (zeros at the start = the one-shot zero padding), the last input row of every 2-tap
+    transposed conv, the transformer's K/V caches (positions 0.. of this decode, window 72).  The per-row math is
+    the one-shot's; only the GEMM row counts differ (results equal up to fp summation order).
+    """
+
+    def __init__(self, dec: CodecDecoder, B: int, max_frames: int):
+        self.dec, self.B, self.max_frames = dec, B, max_frames
+        d, dev = dec.d, dec.dev
+        self.nf = 0  # frames fed
+        self.kc = [torch.zeros(B, dec.kvh, max_frames, dec.hd, dtype=torch.float32, device=dev) for _ in dec.layers]
+        self.vc = [torch.zeros_like(k) for k in self.kc]
+        if dec.cos.shape[0] < max_frames:
+            dec.cos, dec.sin = K.rope_tables(dec.hd, d["rope_theta"], max_frames + 64, dev)
+        self.hist = {}  # stage key -> [B][rows][C] input history
+        self.pcm = torch.zeros(B, dec.total_upsample * max_frames, dtype=torch.float32, device=dev)
+        self.ns = 0  # valid samples in self.pcm
+
+    # -- stages ----------------------------------------------------------------------------------------
+    def _causal(self, key, x, n, Wt, cin, out=None, epi=_hip.EPI_STORE, snake=None):
+        """x [B][n][cin] new input rows -> [B][n][Wt.N] outputs of the causal conv (history = previous inputs)."""
+        dec, B = self.dec, self.B
+        H = (Wt.taps - 1) * getattr(Wt, "dil", 1)
+        if H:
+            h = self.hist.get(key)
+            if h is None:
+                h = torch.zeros(B, H, cin, dtype=x.dtype, device=x.device)
+            xin = torch.cat([h, x.view(B, n, cin)], 1).contiguous()
+            self.hist[key] = xin[:, -H:].clone()
+        else:
+            xin = x
+        if out is None:
+            out = torch.empty(B * n, Wt.N, dtype=dec.adt, device=dec.dev)
+        dec._conv(xin, Wt, B, H + n, n, 0, out, cin, epi=epi, snake=snake)
+        return out
+
+    def _tconv2(self, key, x, n, Wt, cin, snake):
+        """2-tap transposed conv (row t <- inputs t, t + 1): returns (rows out, [B*rows][Wt.N])."""
+        dec, B = self.dec, self.B
+        h = self.hist.get(key)
+        xin = x.view(B, n, cin) if h is None else torch.cat([h, x.view(B, n, cin)], 1)
+        xin = xin.contiguous()
+        L = xin.shape[1]
+        self.hist[key] = xin[:, -1:].clone()
+        rows = L - 1
+        out = torch.empty(B * max(rows, 0), Wt.N, dtype=dec.adt, device=dec.dev)
+        if rows > 0:
+            dec._conv(xin, Wt, B, L, rows, 0, out, cin, snake=snake)
+        return rows, out
+
+    def _transformer(self, h, n):
+        dec, B, dev = self.dec, self.B, self.dec.dev
+        R, p0 = B * n, self.nf
+        hid, nh, nkv, D = dec.hid, dec.heads, dec.kvh, dec.hd
+        x = torch.empty(R, dec.inp.N, dtype=torch.float32, device=dev)
+        K.gemm(h, dec.inp, x, R, dec.lat, dec.inp.N)
+        pos = torch.arange(p0, p0 + n, device=dev, dtype=torch.int32).repeat(B)
+        meta_b = torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(n)
+        row_len, row_start = pos + 1, torch.zeros_like(pos)
+        qkv_w = (nh + 2 * nkv) * D
+        qkv = torch.empty(R, qkv_w, dtype=torch.float32, device=dev)
+        q = torch.empty(R, nh * D, dtype=torch.float32, device=dev)
+        att = torch.empty(R, nh * D, dtype=torch.float32, device=dev)
+        inter = dec.d["intermediate_size"]
+        hmid = torch.empty(R, inter, dtype=torch.float32, device=dev)
+        eps, win, Lm = dec.d["rms_norm_eps"], dec.d["sliding_window"], self.max_frames
+        for L, kc, vc in zip(dec.layers, self.kc, self.vc):
+            K.gemm(x, L["qkv"], qkv, R, hid, qkv_w, rms=True, eps=eps)
+            K.qkv_post(qkv, R, nh, nkv, D, None, None, eps, dec.cos, dec.sin, pos, meta_b, pos, q, kc, vc, Lm)
+            K.attention(q, R, nh, nkv, D, kc, vc, Lm, meta_b, row_start, row_len, att, min(win, p0 + n), window=win)
+            K.gemm(att, L["o"], x, R, nh * D, hid, colscale=L["ls1"], epi=_hip.EPI_ADD)
+            K.gemm(x, L["gu"], hmid, R, hid, inter, rms=True, eps=eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(hmid, L["down"], x, R, inter, hid, colscale=L["ls2"], epi=_hip.EPI_ADD)
+        y = torch.empty(R, dec.lat, dtype=dec.adt, device=dev)
+        K.gemm(x, dec.outp, y, R, hid, dec.lat, rms=True, eps=eps)
+        return y
+
+    # -- feeding ---------------------------------------------------------------------------------------
+    def feed(self, codes: torch.Tensor) -> int:
+        """codes int [B, n, 16] (the next n frames) -> number of valid samples now in self.pcm."""
+        dec, B, dev, adt = self.dec, self.B, self.dec.dev, self.dec.adt
+        n = codes.shape[1]
+        if n == 0:
+            return self.ns
+        if self.nf + n > self.max_frames:
+            raise ValueError(f"CodecStream holds {self.max_frames} frames; {self.nf} fed, {n} more given")
+        codes = codes.to(dev, torch.int32).contiguous()
+        # C1 (per frame)
+        o1 = torch.empty(B * n, dec.cb_dim, dtype=torch.float32, device=dev)
+        o2 = torch.empty_like(o1)
+        K.rvq_gather(dec.tables, codes.shape[2], 1, dec.tables.shape[1], dec.cb_dim, codes, B, n, o1, o2)
+        cd = dec.proj_first.N
+        h = torch.empty(B * n, cd, dtype=adt, device=dev)
+        K.gemm(o1, dec.proj_first, h, B * n, dec.cb_dim, cd)
+        K.gemm(o2, dec.proj_rest, h, B * n, dec.cb_dim, cd, epi=_hip.EPI_ADD)
+        # C2, C3
+        x = self._causal("pre", h, n, dec.pre_conv, cd)
+        x = self._transformer(x, n)
+        self.nf += n
+        # C4: upsample (1-tap transposed conv, no state) + ConvNeXt (causal depthwise k=7 + LayerNorm, then per row)
+        L, C = n, dec.lat
+        for i, u in enumerate(dec.ups):
+            f = u["f"]
+            y = torch.empty(B * L * f, C, dtype=adt, device=dev)
+            dec._conv(x, u["tconv"], B, L, L, 0, y, C)
+            L *= f
+            Hd = u["dw_w"].shape[1] - 1
+            hkey = f"dw{i}"
+            hst = self.hist.get(hkey)
+            if hst is None:
+                hst = torch.zeros(B, Hd, C, dtype=adt, device=dev)
+            yin = torch.cat([hst, y.view(B, L, C)], 1).contiguous()
+            self.hist[hkey] = yin[:, -Hd:].clone()
+            z = torch.empty_like(yin)
+            K.dwconv_ln(yin, B, Hd + L, C, u["dw_w"], u["dw_b"], u["ln_w"], u["ln_b"], 1e-6, z)
+            z = z[:, Hd:].contiguous()
+            hmid = torch.empty(B * L, u["pw1"].N, dtype=adt, device=dev)
+            K.gemm(z, u["pw1"], hmid, B * L, C, u["pw1"].N, act=_hip.ACT_GELU)
+            K.gemm(hmid, u["pw2"], y, B * L, u["pw1"].N, C, colscale=u["gamma"], epi=_hip.EPI_ADD)
+            x = y
+        # C5
+        x = self._causal("conv0", x, L, dec.conv0, C)
+        C = dec.d["decoder_dim"]
+        # C6
+        for bi, blk in enumerate(dec.blocks):
+            r, cout = blk["r"], blk["cout"]
+            rows, y = self._tconv2(f"t{bi}", x, L, blk["tconv"], C, blk["s"])
+            L, C, x = rows * r, cout, y
+            if L == 0:
+                return self.ns
+            for ui, un in enumerate(blk["units"]):
+                bb = self._causal(f"u{bi}.{ui}", x, L, un["c1"], C, snake=un["s1"])
+                self._causal(f"v{bi}.{ui}", bb, L, un["c2"], C, out=x, epi=_hip.EPI_ADD, snake=un["s2"])
+        # C7
+        out = self._causal("last", x, L, dec.conv_last, C, out=torch.empty(B * L, dec.conv_last.N, dtype=torch.float32,
+                                                                            device=dev), snake=dec.s_last)
+        pcm = out[:, 0].contiguous()
+        K.clamp_pcm(pcm, pcm.numel(), pcm)
+        self.pcm[:, self.ns:self.ns + L] = pcm.view(B, L)
+        self.ns += L
+        return self.ns

@@ -335,13 +335,14 @@ class Qwen3TTSModel:
 
     @torch.no_grad()
     def stream(self, text, speaker=None, language=None, instruct=None, non_streaming_mode=True,
-               first_chunk_frames=4, chunk_frames=48, left_context=25, **kwargs):
+               first_chunk_frames=4, chunk_frames=48, left_context=None, **kwargs):
         """New surface (no reference counterpart): streaming custom-voice generation.
         Yields (utterance index, pcm chunk np.float32, sample rate, is_last) while the batch decodes: the first
         chunk after `first_chunk_frames` frames (4 frames = 0.32 s of audio: the first packet arrives after prefill + 5
         decode frames), then every `chunk_frames`.  Per utterance the
-        chunks concatenate to the one-shot generate_custom_voice() length; codes are identical to it (see
-        TTSModel.stream for the chunk / left-context rule)."""
+        chunks concatenate to the one-shot generate_custom_voice() length and equal its PCM up to fp summation order
+        (a stateful incremental codec decode; codes are identical -- see TTSModel.stream for the chunk rule and the
+        stateless `left_context` form)."""
         input_ids, ins_ids, languages, speakers = self._custom_voice_inputs(text, speaker, language, instruct)
         sr = self.model.speech_tokenizer.get_output_sample_rate()
         for i, pcm, last in self.model.stream(input_ids=input_ids, instruct_ids=ins_ids, languages=languages,

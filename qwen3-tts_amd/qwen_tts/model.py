@@ -179,17 +179,19 @@ class TTSModel:
                speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
-               first_chunk_frames=4, chunk_frames=48, left_context=325, use_graph=True, **kwargs):
+               first_chunk_frames=4, chunk_frames=48, left_context=None, use_graph=True, **kwargs):
         """Streaming generation (the reference has none): yields (row, pcm, last) as frames finish.
 
         Per row the chunks concatenate to the one-shot generate() + decode() PCM (Z:259-365): the reference
         decodes the zero-right-padded batch in 300-frame chunks with 25 frames of left context, dropping the
         last 555 samples of each chunk (no next frame), and keeps 1920 x #nonzero-cb0 samples.  A streamed
-        window [s, e) never crosses a chunk boundary and is decoded from its chunk's start (minus those 25
-        context frames) plus one lookahead frame, so it reproduces that output up to fp rounding.
-        `left_context` < 325 caps the re-decoded history per window (less work, approximate: in fp32 150 frames
-        -> rel-L2 1e-6, 72 -> 7e-4, 25 -> 2e-2; tools/stream_fidelity.py).  Codes are identical to generate().
-        pcm is a 1-D fp32 device tensor of 24 kHz samples."""
+        window [s, e) never crosses a chunk boundary and needs one lookahead frame.  Default (left_context=None):
+        one stateful incremental decoder per reference chunk (codec.CodecStream, primed with the chunk's 25 context
+        frames) is fed each frame once, so every sample is computed once and equals the one-shot output up to fp
+        summation order.  An int `left_context` selects the stateless form instead: each window is re-decoded from
+        min(its chunk's start, left_context frames back) -- 325 reproduces the reference, less is approximate (in
+        fp32 150 frames -> rel-L2 1e-6, 72 -> 7e-4, 25 -> 2e-2; tools/stream_fidelity.py).  Codes are identical to
+        generate().  pcm is a 1-D fp32 device tensor of 24 kHz samples."""
         dec = self.speech_tokenizer.model
         up = dec.total_upsample
         RC, RX = self.REF_CHUNK, self.REF_CTX
@@ -206,6 +208,7 @@ class TTSModel:
         cum = [0] * B                     # samples emitted per row
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames + 1)
+        cs, cs_k, cs_fed = None, -1, 0    # stateful decoder of reference chunk cs_k, fed frames [.., cs_fed)
         for sessions, frames, final in it:
             # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
             codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
@@ -228,13 +231,24 @@ class TTSModel:
                 e = min(target, cend)
                 closed = e == cend or e == t_end  # this reference chunk ends at e
                 base = k * RC - (RX if k * RC - RX > 0 else k * RC)
-                ctx = min(emitted - base, left_context)
                 hi = e if closed else e + 1
-                cc = codes[:, emitted - ctx:hi].clone()
+                if left_context is None:
+                    if cs_k != k:  # a new reference chunk: a fresh decoder, primed from the chunk's context frames
+                        cs, cs_k, cs_fed = dec.stream(B, RX + RC), k, base
+                    lo, ctx = cs_fed, emitted - base
+                else:
+                    ctx = min(emitted - base, left_context)
+                    lo = emitted - ctx
+                cc = codes[:, lo:hi].clone()
                 for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
                     if end[b] is not None and end[b] < hi:
-                        cc[b, max(end[b] - (emitted - ctx), 0):] = 0
-                w = dec.forward(cc)
+                        cc[b, max(end[b] - lo, 0):] = 0
+                if left_context is None:
+                    cs.feed(cc)
+                    cs_fed = hi
+                    w = cs.pcm
+                else:
+                    w = dec.forward(cc)
                 n = up * (e - emitted) - (555 if closed else 0)
                 for b in range(B):
                     if done[b]:
