@@ -767,6 +767,17 @@ void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
   else launch_gemv_u<WT, AT, OT, WPB, 4>(p, nt, s);
 }
 
+// largest row count run as the decode GEMV over row groups of gemv_mr() rows (QT_GEMV_MAX_M / QT_GEMV_MR override,
+// measurement; 16 = decode only)
+inline int gemv_max_m() {
+  static const int v = [] { const char* e = getenv("QT_GEMV_MAX_M"); return e ? atoi(e) : 256; }();
+  return v;
+}
+inline int gemv_mr() {
+  static const int v = [] { const char* e = getenv("QT_GEMV_MR"); return e ? atoi(e) : 16; }();
+  return std::max(1, std::min(16, v));
+}
+
 // smallest row count routed to the LDS-tiled implicit GEMM (QT_IGEMM_MIN_M overrides, measurement)
 inline int igemm_min_m() {
   static const int v = [] { const char* e = getenv("QT_IGEMM_MIN_M"); return e ? atoi(e) : 128; }();
@@ -777,7 +788,7 @@ template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
-  if (p.M <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr && !p.a_elu) {
+  if (p.mr <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr && !p.a_elu) {
     const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
     if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
     else if (kts >= 16 && p.wpb_max >= 8) launch_gemv<WT, AT, OT, 8>(p, nt, (kts + 7) / 8, s);
@@ -918,6 +929,17 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
       // CP down 5.8 -> 5.6 us (o_proj / lm_head keep 16)
       if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
     }
+  } else if ((a->M <= 96 || (a->M <= gemv_max_m() && a->N <= 2048)) && a->taps == 0 && a->w_dtype == QT_BF16 &&
+             a->K % KT == 0 && a->gamma == nullptr && a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr) {
+    // skinny GEMM (17..96 rows, or up to gemv_max_m rows of a <= 2048-column output: the talker prefill of
+    // streaming-text prompts, short codec windows): the decode GEMV over row groups of 16 -- one block per (column
+    // tile, row group), the weight tile streamed from HBM once and re-read from L2 by the other row groups of its
+    // XCD.  Its time grows with the row groups; the tiled GEMMs' is flat in M but their grids are small for narrow
+    // outputs (tools/prefill_gemm_bench.py: M=80 o 29.6 -> 12.2 us, down 93.7 -> 29.0, qkv 36.0 -> 30.0, gate-up
+    // 79.0 -> 65.4; at M=160 gate-up 86 (igemm) vs 130, down 233 vs 48)
+    p.mr = gemv_mr();
+    p.ks = 1;
+    if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
   }
   hipStream_t s = (hipStream_t)stream;
   const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;

@@ -1,5 +1,6 @@
 """Talker prefill linears at streaming-text prompt sizes (M = 8 x ~10 rows), 1.7B dims: per-launch time of each
-shape on the path qt_gemm picks (QT_IGEMM_MIN_M moves the implicit-GEMM threshold for A/B)."""
+shape on the path qt_gemm picks (QT_IGEMM_MIN_M moves the implicit-GEMM threshold, QT_GEMV_MAX_M the row-grouped
+decode GEMV's, for A/B)."""
 import os
 import sys
 import torch
@@ -14,7 +15,7 @@ dev = torch.device("cuda:0")
 def main():
     shapes = [("qkv", 4096, 2048, True, 0, torch.float32), ("o", 2048, 2048, False, 1, torch.bfloat16),
               ("gate-up", 12288, 2048, True, 2, torch.float32), ("down", 2048, 6144, False, 1, torch.bfloat16)]
-    for M in (80, 160):
+    for M in (24, 48, 80, 112, 160, 256):
         for name, N, Kk, rms, epi, adt in shapes:
             nmat = max(2, int(600e6 // (N * Kk * 2)))
             Ws = [K.tile_linear(torch.randn(N, Kk, device=dev) * 0.02, torch.bfloat16) for _ in range(nmat)]
@@ -25,8 +26,7 @@ def main():
             it = {"i": 0}
 
             def f():
-                K.gemm(A, Ws[it["i"] % nmat], o, M, Kk, o.shape[1] if ep != _hip.EPI_SWIGLU else N, rms=rms,
-                       eps=1e-6, epi=ep)
+                K.gemm(A, Ws[it["i"] % nmat], o, M, Kk, o.shape[1], rms=rms, eps=1e-6, epi=ep)
                 it["i"] += 1
             timed(f, f"prefill {name} M={M} {N}x{Kk}")
             del Ws
