@@ -188,6 +188,32 @@ typedef struct qt_mlp_args {
   int* err;
 } qt_mlp_args;
 long long qt_mlp_ws_bytes(int M, int H, int I);
+/* ---------------------------------------------------------------------------------------------
+ * qt_cp_mlp: one persistent launch (256 workgroups, one per CU) for a code-predictor decode step's
+ *   x += down(SwiGLU(gate_up(rms(x16))));  x16 = bf16(x);  out3 = rms(x16) . W3
+ * i.e. M:1000-1011 (post-attention RMSNorm, Qwen3TTSTalkerTextMLP, residual) followed by the next RMS-normalised
+ * projection (the next layer's q/k/v, or the final norm + lm_head[g], M:1299), with the two all-to-all hand-offs
+ * (SwiGLU output, new residual) inside the launch as tagged granules instead of kernel boundaries.  bf16 weight
+ * tiles from qt_tile_weight (w_gu gate/up interleaved 8 + 8 rows per tile, RMSNorm gammas folded into w_gu / w3).
+ * M <= 16 rows; H = 1024, I = 3072, N3 in {1024, 2048, 4096} (qt_cp_mlp_supported; needs >= 256 CUs).
+ * tags: device scratch of qt_cp_mlp_tags_bytes(H, I), zeroed before the first launch of a tag sequence; the launch's
+ * tag base is *epoch_ctr * epoch_mul + epoch_add (>= 1, distinct for every launch until the scratch is zeroed
+ * again).  err: device int set to 1 if a hand-off wait timed out (results are then invalid; never hangs).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct qt_cp_mlp_args {
+  int M, H, I, N3;
+  void* x16; long long ldx16;        /* bf16 residual shadow: read (gate/up A operand), rewritten with the new rows */
+  float* x; long long ldx;           /* fp32 residual, += the down projection */
+  const void* w_gu; const void* w_down; const void* w3;
+  float eps;
+  float* out3; long long ldo3;
+  void* tags; long long tags_bytes;
+  const int* epoch_ctr; int epoch_mul, epoch_add;
+  int* err;
+} qt_cp_mlp_args;
+long long qt_cp_mlp_tags_bytes(int H, int I);
+int qt_cp_mlp_supported(int M, int H, int I, int N3);
+int qt_cp_mlp(const qt_cp_mlp_args* args, void* stream);
 int qt_mlp_decode(const qt_mlp_args* args, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

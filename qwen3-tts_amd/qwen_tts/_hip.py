@@ -88,13 +88,20 @@ class MlpArgs(ctypes.Structure):
                 ("w_down", c_void_p), ("eps", c_float), ("ws", c_void_p), ("ws_bytes", c_ll), ("err", c_void_p)]
 
 
+class CpMlpArgs(ctypes.Structure):
+    _fields_ = [("M", c_int), ("H", c_int), ("I", c_int), ("N3", c_int), ("x16", c_void_p), ("ldx16", c_ll),
+                ("x", c_void_p), ("ldx", c_ll), ("w_gu", c_void_p), ("w_down", c_void_p), ("w3", c_void_p),
+                ("eps", c_float), ("out3", c_void_p), ("ldo3", c_ll), ("tags", c_void_p), ("tags_bytes", c_ll),
+                ("epoch_ctr", c_void_p), ("epoch_mul", c_int), ("epoch_add", c_int), ("err", c_void_p)]
+
+
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj",
            "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
-           "qt_scale_add", "qt_bcast_rows"]
+           "qt_scale_add", "qt_bcast_rows", "qt_cp_mlp", "qt_cp_mlp_tags_bytes", "qt_cp_mlp_supported"]
 
 _LIB = None
 
@@ -121,6 +128,7 @@ def load_library(path: str = LIB_PATH):
         "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
         "qt_decode_attn_oproj": [P, P],
+        "qt_cp_mlp": [P, P], "qt_cp_mlp_tags_bytes": [c_int, c_int], "qt_cp_mlp_supported": [c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],
@@ -134,7 +142,7 @@ def load_library(path: str = LIB_PATH):
     for name, args in sig.items():
         f = getattr(L, name)
         f.argtypes = args
-        f.restype = c_ll if name.endswith("_ws_bytes") else c_int
+        f.restype = c_ll if name.endswith("_ws_bytes") or name.endswith("_tags_bytes") else c_int
     return L
 
 

@@ -186,6 +186,29 @@ def mlp_decode(x, M, H, I, w_gu: "Tiled", w_down: "Tiled", eps, ws, err=None):
     check(_hip.lib().qt_mlp_decode(ctypes.byref(a), stream()), "qt_mlp_decode")
 
 
+def cp_mlp_tags_bytes(H, I):
+    return int(_hip.lib().qt_cp_mlp_tags_bytes(H, I))
+
+
+def cp_mlp_supported(M, H, I, N3) -> bool:
+    return bool(_hip.lib().qt_cp_mlp_supported(M, H, I, N3))
+
+
+def cp_mlp(x16, x, M, H, I, w_gu: "Tiled", w_down: "Tiled", w3: "Tiled", out3, eps, tags, epoch_ctr, epoch_add, err,
+           epoch_mul=0):
+    """qt_cp_mlp (one persistent launch): x[:M] += down(SwiGLU(gate_up(rms(x16)))); x16 = bf16(x);
+    out3[:M] = rms(x16) . w3.  tags: zeroed uint8 scratch of cp_mlp_tags_bytes(H, I); the launch's tag base is
+    epoch_ctr[0] * epoch_mul + epoch_add (distinct per launch until tags is zeroed again)."""
+    a = _hip.CpMlpArgs()
+    a.M, a.H, a.I, a.N3 = M, H, I, w3.N
+    a.x16, a.ldx16, a.x, a.ldx = ptr(x16), x16.stride(0), ptr(x), x.stride(0)
+    a.w_gu, a.w_down, a.w3, a.eps = ptr(w_gu.w), ptr(w_down.w), ptr(w3.w), eps
+    a.out3, a.ldo3 = ptr(out3), out3.stride(0)
+    a.tags, a.tags_bytes = ptr(tags), tags.numel() * tags.element_size()
+    a.epoch_ctr, a.epoch_mul, a.epoch_add, a.err = ptr(epoch_ctr), epoch_mul, epoch_add, ptr(err)
+    check(_hip.lib().qt_cp_mlp(ctypes.byref(a), stream()), "qt_cp_mlp")
+
+
 def qkv_post(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, q_out, kc, vc, Lmax):
     a = _hip.QkvArgs()
     a.R, a.Hq, a.Hkv, a.D = R, Hq, Hkv, D

@@ -63,22 +63,25 @@ class _Stack:
         if self.cos.shape[0] < npos:
             self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
 
-    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None, qkv0=False):
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None, qkv0=False, mlp=None):
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
         decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention.
         x16 (bf16 mode, R <= 16): bf16 shadow of x, kept current by every writer of x (the residual-add epilogues
         store both) and read as the A operand of the RMS-normalised GEMVs (QKV, gate/up): their MFMA rounds A to
         bf16 anyway, so only the RMS row sums change (they come from the bf16 values, as the reference's bf16
         residual stream gives them) while the activation fetch halves.
-        qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler)."""
+        qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler).
+        mlp (code-predictor decode, bf16 + x16): {"tags", "ctr", "err", "base", "head": (W, out)} -- each layer's MLP
+        and the next RMS GEMV (next layer's q/k/v, or the head W into out) as one persistent qt_cp_mlp launch."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
         if x16 is not None and ("mlp_ws" in scratch or R > 16):
             x16 = None  # the fused MLP / prefill GEMMs write x only
         xa = x if x16 is None else x16
+        use_mlp = mlp is not None and fused_ao and x16 is not None and R <= 16
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            if not (qkv0 and li == 0):
+            if not (qkv0 and li == 0) and not (use_mlp and li > 0):
                 K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
@@ -97,7 +100,11 @@ class _Stack:
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             if not fused_ao:
                 K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD, out2=x16)
-            if "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
+            if use_mlp:  # gate/up -> down -> the next RMS GEMV in one persistent launch
+                w3, o3 = (self.layers[li + 1].qkv, scratch["qkv"]) if li + 1 < len(self.layers) else mlp["head"]
+                K.cp_mlp(x16, x, R, self.H, self.I, L.gu, L.down, w3, o3, self.eps, mlp["tags"], mlp["ctr"],
+                         mlp["base"] + li, mlp["err"])
+            elif "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
                 K.mlp_decode(x, R, self.H, self.I, L.gu, L.down, self.eps, scratch["mlp_ws"], scratch["mlp_err"])
             else:
                 K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
@@ -115,6 +122,11 @@ ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
 QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
+# code-predictor decode MLP + next RMS GEMV as one persistent launch (qt_cp_mlp, bf16 mode; QT_CP_MLP=1): correct
+# and tested, but measured slower than the three GEMV launches it replaces (16.5 vs 13.9 us per layer, CP step 122
+# vs 110 us; profiles/r02_cp_mlp_persistent_ab.txt): each in-launch tagged hand-off costs as much as the kernel
+# boundary it removes, so it is opt-in
+CP_MLP = os.environ.get("QT_CP_MLP", "0") == "1"
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -162,6 +174,12 @@ class CPLane:
         p2 = torch.arange(2 * nb, device=dev, dtype=torch.int32) % 2
         self.meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * nb),
                       "row_batch": rb2, "small_T": 2}
+        # persistent code-predictor MLP (qt_cp_mlp, bf16 mode): hand-off tag buffer (zeroed once per frame), a zero
+        # epoch word (the tag base is a per-launch constant of the frame graph) and the time-out flag
+        self.mlp = None
+        if self.x16 is not None and eng.cp_mlp_ok(nb):
+            self.mlp = {"tags": torch.zeros(K.cp_mlp_tags_bytes(c.H, c.I), dtype=torch.uint8, device=dev),
+                        "ctr": i32(1), "err": i32(1)}
         rb = torch.arange(nb, dtype=torch.int32, device=dev)
         self.meta = []
         for g in range(1, s.G - 1):
@@ -306,6 +324,14 @@ class TalkerEngine:
         self._cp_streams: List[torch.cuda.Stream] = []
         torch.cuda.synchronize()
 
+    def cp_mlp_ok(self, rows: int) -> bool:
+        """qt_cp_mlp serves this code predictor's decode steps at `rows` rows (bf16 weights, fused attention + o_proj,
+        supported dims, >= 256 CUs); QT_CP_MLP=0 keeps the launch-per-GEMV form (A/B measurement)."""
+        c = self.cp
+        return (CP_MLP and self.wdt == torch.bfloat16 and _attn_oproj_ok(c) and ATTN_OPROJ
+                and K.cp_mlp_supported(rows, c.H, c.I, c.qkv_w) and K.cp_mlp_supported(rows, c.H, c.I, self.Vc)
+                and all(L.gu.dtype == torch.bfloat16 for L in c.layers))
+
     def _proj_table(self, emb, Hc):
         """small_to_mtp(embedding table) (M:1299 applied row-wise) or the table itself, fp32 [V][Hc]."""
         V = emb.shape[0]
@@ -444,16 +470,22 @@ class TalkerEngine:
         p16 = ln.x16 if 2 * nb <= 16 else None  # forward() keeps the shadow for decode-GEMV row counts only
         c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
         self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
+        if ln.mlp is not None:
+            ln.mlp["tags"].zero_()  # tag bases below are per-launch constants, distinct within one frame
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
             x16 = None if ln.x16 is None else ln.x16[:nb]
+            mlp = None
+            if ln.mlp is not None:
+                mlp = dict(ln.mlp, base=1 + (g - 1) * len(c.layers), head=(self.lm_heads[g], ln.logits))
             c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16,
-                      qkv0=self.cp_qkv_tabs is not None)
-            self._cp_head(s, ln, x, Hc, g, x16)
+                      qkv0=self.cp_qkv_tabs is not None, mlp=mlp)
+            self._cp_head(s, ln, x, Hc, g, x16, logits_ready=mlp is not None)
 
-    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None):
+    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None, logits_ready=False):
         c, gp = self.cp, s.gp
-        K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
+        if not logits_ready:  # (else the last layer's qt_cp_mlp launch computed them)
+            K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed_ptr=s.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
@@ -558,6 +590,10 @@ class TalkerEngine:
             for sc in [s.sc_t] + [ln.sc for ln in s.cp_lanes]:
                 if "mlp_err" in sc and int(sc["mlp_err"].item()):
                     raise RuntimeError("qt_mlp_decode: in-kernel arrival wait timed out (results invalid)")
+            for ln in s.cp_lanes:
+                if ln.mlp is not None and int(ln.mlp["err"].item()):
+                    ln.mlp["err"].zero_()
+                    raise RuntimeError("qt_cp_mlp: an in-launch hand-off wait timed out (results invalid)")
         yield sessions, frames, True
 
     def collect(self, sessions, frames):

@@ -1040,3 +1040,80 @@ def test_codec_decode_matches_reference(fname, preset, dtype):
             else:
                 rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
                 assert rel < 5e-2, (key, rel)
+
+
+@pytest.mark.parametrize("M,N3", [(8, 4096), (8, 2048), (5, 4096), (16, 4096), (1, 2048), (16, 2048)])
+def test_cp_mlp_matches_gemv_chain(M, N3):
+    """qt_cp_mlp (persistent launch: gate/up + SwiGLU -> down + residual -> next RMS GEMV, in-launch tagged hand-offs)
+    == the three decode GEMVs it replaces (same bf16 operand roundings; fp32 summation order differs), over
+    consecutive launches with increasing tags, and no hand-off time-out."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    H, I = 1024, 3072
+    if not Kn.cp_mlp_supported(M, H, I, N3):
+        pytest.skip("needs >= 256 CUs")
+    g = torch.Generator().manual_seed(M * 31 + N3)
+    gam1, gam2 = 1 + 0.1 * torch.randn(H, generator=g), 1 + 0.1 * torch.randn(H, generator=g)
+    wg, wu = torch.randn(I, H, generator=g) * 0.03, torch.randn(I, H, generator=g) * 0.03
+    wd = torch.randn(H, I, generator=g) * 0.02
+    w3 = torch.randn(N3, H, generator=g) * 0.03
+    gu = Kn.tile_swiglu(wg.to(dev), wu.to(dev), torch.bfloat16, gamma=gam1.to(dev))
+    dn = Kn.tile_linear(wd.to(dev), torch.bfloat16)
+    t3 = Kn.tile_linear(w3.to(dev), torch.bfloat16, gamma=gam2.to(dev))
+    x0 = torch.randn(M, H, generator=g).to(dev)
+    tags = torch.zeros(Kn.cp_mlp_tags_bytes(H, I), dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+    # reference chain (three decode GEMVs), twice in a row
+    xr, x16r = x0.clone(), x0.to(torch.bfloat16)
+    h = torch.empty(M, I, dtype=torch.bfloat16, device=dev)
+    o_ref = []
+    for _ in range(2):
+        Kn.gemm(x16r, gu, h, M, H, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU, splitk=1)
+        Kn.gemm(h, dn, xr, M, I, H, epi=_hip.EPI_ADD, out2=x16r, splitk=1)
+        o = torch.empty(M, N3, device=dev)
+        Kn.gemm(x16r, t3, o, M, H, N3, rms=True, eps=1e-6, splitk=1)
+        o_ref.append(o)
+    xf, x16f = x0.clone(), x0.to(torch.bfloat16)
+    o_f = []
+    for i in range(2):
+        o = torch.empty(M, N3, device=dev)
+        Kn.cp_mlp(x16f, xf, M, H, I, gu, dn, t3, o, 1e-6, tags, ctr, i + 1, err)
+        o_f.append(o)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    # a different fp32 summation order flips an occasional bf16 rounding of h / x16 (one bf16 ulp): compare in rel-L2
+    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())  # noqa: E731
+    assert rel(xf - x0, xr - x0) < 2e-3, rel(xf - x0, xr - x0)
+    assert rel(x16f, x16r) < 4e-3
+    for a, b in zip(o_f, o_ref):
+        assert rel(a, b) < 1e-2, rel(a, b)
+
+
+def test_cp_mlp_pipeline_tracks_launch_path(monkeypatch):
+    """The opt-in persistent CP MLP (talker.CP_MLP) in the full bf16 frame graph at the 1.7B CP dims: the first frame's
+    greedy codes equal the launch-per-GEMV path's (bf16 summation-order differences may flip a later near-tie of the
+    synthetic weights' flat logits, after which the continuations differ)."""
+    from qwen_tts import talker as T
+    from qwen_tts.model import TTSModel
+    from qwen_tts.weights import read_json, resolve_path, synthetic, talker_specs
+    dev = _dev()
+    d = resolve_path("synthetic:1.7b-customvoice")
+    cfg = read_json(os.path.join(d, "config.json"))
+    W = synthetic(talker_specs(cfg), dev)  # seeded synthetic weights generated on the device
+    ids = [[151644, 77091, 198] + list(range(1000, 1020)) + [151645, 198, 151644, 77091, 198]] * 2
+    kw = dict(input_ids=ids, languages=["english"] * 2, speakers=["vivian"] * 2, non_streaming_mode=False,
+              max_new_tokens=6, do_sample=False, subtalker_dosample=False)
+    out = {}
+    for on in (False, True):
+        monkeypatch.setattr(T, "CP_MLP", on)
+        m = TTSModel(cfg, W, dtype="bf16")
+        if on:
+            assert m.engine.cp_mlp_ok(2)
+        codes, _ = m.generate(**kw)
+        out[on] = codes
+        del m
+        torch.cuda.empty_cache()
+    for a, b in zip(out[False], out[True]):
+        assert a.shape == b.shape
+        assert torch.equal(a[0], b[0])  # later codes may follow a flipped near-tie into a different continuation
