@@ -233,7 +233,7 @@ class TTSModel:
                speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
-               first_chunk_frames=4, chunk_frames=48, left_context=None, use_graph=True, **kwargs):
+               first_chunk_frames=2, chunk_frames=48, left_context=None, use_graph=True, **kwargs):
         """Streaming generation (the reference has none): yields (row, pcm, last) as frames finish.
 
         Per row the chunks concatenate to the one-shot generate() + decode() PCM (Z:259-365): the reference
@@ -260,8 +260,10 @@ class TTSModel:
         cap = [None] * B                  # one-shot sample count (1920 x #nonzero cb0) once the row has ended
         done = [False] * B
         cum = [0] * B                     # samples emitted per row
+        # chunk sizes double from first_chunk_frames up to chunk_frames: each chunk's audio (80 ms per frame) covers
+        # the generation of the next one (~3 ms per frame), so playback started at the first packet never starves
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
-                                     first=first_chunk_frames + 1)
+                                     first=first_chunk_frames + 1, grow=True)
         cs, cs_k, cs_fed = None, -1, 0    # stateful decoder of reference chunk cs_k, fed frames [.., cs_fed)
         for sessions, frames, final in it:
             # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)

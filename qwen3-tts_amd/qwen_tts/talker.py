@@ -513,9 +513,10 @@ class TalkerEngine:
         return out
 
     def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
-                    groups: Optional[int] = None, every: int = 0, first: int = 0):
+                    groups: Optional[int] = None, every: int = 0, first: int = 0, grow: bool = False):
         """Prefill + frame loop as a generator: yields (sessions, frames_done, final) after `first` frames, then
-        every `every` frames (0: only at the end), and once at the end with final=True.  codes[:, :frames_done]
+        every `every` frames (0: only at the end; grow=True: intervals double from first - 1 up to `every`), and once
+        at the end with final=True.  codes[:, :frames_done]
         of every session are final when yielded (device; the yield synchronises the row-group streams), and
         codes[:, frames_done, 0] already holds the next frame's cb0 (EOS of rows that just finished)."""
         B, P, H = embeds.shape
@@ -537,15 +538,16 @@ class TalkerEngine:
                     if max_frames > 0 and use_graph and s.graph is None:
                         s.graph = self._capture(s)
                 streams.append(st)
-            yield from self._frames(sessions, streams, max_frames, use_graph, on_frames, every, first)
+            yield from self._frames(sessions, streams, max_frames, use_graph, on_frames, every, first, grow)
         finally:
             self.release(sessions)
 
-    def _frames(self, sessions, streams, max_frames, use_graph, on_frames, every, first):
+    def _frames(self, sessions, streams, max_frames, use_graph, on_frames, every, first, grow=False):
         main = torch.cuda.current_stream(self.dev)
         frames = 0
         check_every = 8
         next_yield = first or every
+        interval = max(first - 1, 1)
         for s, st in zip(sessions, streams):
             with torch.cuda.stream(st):
                 s.hiddens[:, 0].copy_(s.past_hidden)  # later frames are recorded inside the frame graph
@@ -567,7 +569,8 @@ class TalkerEngine:
                 for st in streams:
                     main.wait_stream(st)
                 yield sessions, frames, False
-                next_yield = frames + every if every else 0
+                interval = min(every, 2 * interval) if grow else every
+                next_yield = frames + interval if every else 0
             if frames % check_every == 0 and frames < max_frames:
                 flags = []
                 for s, st in zip(sessions, streams):

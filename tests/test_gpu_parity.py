@@ -870,6 +870,30 @@ def test_stream_matches_one_shot(tiny_models, ctx, eos, frames):
             np.testing.assert_allclose(got, w, atol=2e-4, rtol=0)
 
 
+def test_stream_chunk_schedule_grows(tiny_models):
+    """stream() chunks double from first_chunk_frames up to chunk_frames (1, 2, 4, 8, 8, ... frames of 1920
+    samples), so the audio of each chunk outlasts the generation of the next."""
+    from cases import gen_kwargs, make_inputs, talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    from qwen_tts.model import TTSModel
+    _dev()
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype="fp32")
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    model.load_speech_tokenizer(Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer",
+                                                                  dtype="fp32", weights=CW))
+    key = "cv_b2_stream_dialect"
+    case = dict(talker_cases()[key], max_new_tokens=41)
+    ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
+    kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=case["languages"],
+              speakers=case["speakers"], non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+    kw["ignore_eos"] = True
+    sizes = [pcm.numel() for b, pcm, last in model.stream(first_chunk_frames=1, chunk_frames=8, **kw) if b == 0]
+    assert sizes[:5] == [1920 * 1, 1920 * 2, 1920 * 4, 1920 * 8, 1920 * 8], sizes
+
+
 def test_sampling_fresh_seed_per_call_reuses_session(tiny_models):
     """Sampling draws a fresh Philox key per generate() call (like the reference's torch.multinomial): two calls
     give different codes, torch.manual_seed reproduces a call, an explicit seed reproduces itself -- and every
