@@ -127,6 +127,9 @@ QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
 # vs 110 us; profiles/r02_cp_mlp_persistent_ab.txt): each in-launch tagged hand-off costs as much as the kernel
 # boundary it removes, so it is opt-in
 CP_MLP = os.environ.get("QT_CP_MLP", "0") == "1"
+# talker prefill captured into a HIP graph per (session, prompt length) once that length repeats; QT_PREFILL_GRAPH=0
+# always issues it eagerly (A/B)
+PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -263,6 +266,7 @@ class Session:
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox key, read by the captured samplers
         self.row_base = 0
         self.graph = None
+        self.prefill = {}  # prompt length P -> static prefill buffers (+ captured graph once P repeats)
         self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
         nl = max(1, min(eng.cp_lanes, B))
         cuts = [B * i // nl for i in range(nl + 1)]
@@ -638,24 +642,57 @@ class TalkerEngine:
         n_pads = P - n_real
         rope_delta = (max_pos + 1 - n_real).long() - n_pads
         R = B * P
-        pre_meta = {"rope_pos": pos.reshape(-1).to(torch.int32),
-                    "kv_pos": torch.arange(P, device=dev, dtype=torch.int32).repeat(B),
-                    "row_len": torch.arange(1, P + 1, device=dev, dtype=torch.int32).repeat(B),
-                    "row_start": torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])
-                    .reshape(-1).to(torch.int32),
-                    "row_batch": torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(P)}
-        x = embeds.to(dev).float().reshape(R, H).contiguous()
-        t.forward(x, R, pre_meta, s.kv, _scratch(R, t, dev), s.Lmax, P)
-        last = x.view(B, P, H)[:, -1].contiguous()
-        K.rmsnorm(last, t.norm, t.eps, s.past_hidden, B, H)
-        K.gemm(s.past_hidden, self.codec_head, s.logits, B, H, self.V)
-        self._sample_talker(s, s.logits, 0, 99)
+        pre = s.prefill.get(P)
+        if pre is None:  # static buffers of this prompt length (a captured graph binds their addresses)
+            i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
+            pre = {"x": torch.empty(R, H, dtype=torch.float32, device=dev), "sc": _scratch(R, t, dev),
+                   "meta": {"rope_pos": i32(R), "kv_pos": torch.arange(P, device=dev, dtype=torch.int32).repeat(B),
+                            "row_len": torch.arange(1, P + 1, device=dev, dtype=torch.int32).repeat(B),
+                            "row_start": i32(R),
+                            "row_batch": torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(P)},
+                   "last": torch.empty(B, H, dtype=torch.float32, device=dev), "graph": None, "uses": 0}
+            s.prefill[P] = pre
+        pre["meta"]["rope_pos"].copy_(pos.reshape(-1))
+        pre["meta"]["row_start"].copy_(torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])
+                                       .reshape(-1))
+        pre["x"].copy_(embeds.reshape(R, H))
+        if pre["graph"] is not None:
+            pre["graph"].replay()
+        else:
+            self._prefill_compute(s, pre, B, P)
+            pre["uses"] += 1
+            # a prompt length seen twice (streaming-text prompts repeat it: role + codec prefix) gets a captured
+            # prefill: ~170 launches replayed instead of issued from Python (host-bound, ~4.6 ms at B=8)
+            if PREFILL_GRAPH and pre["uses"] >= 2:
+                pre["graph"] = self._capture_prefill(s, pre, B, P)
         # decode counters: step 0, one token generated, pos = P + delta, kv_pos = P, len = P + 1
         s.ctr[1] = 1
         s.meta["rope_pos"].copy_((P + rope_delta).to(torch.int32))
         s.meta["kv_pos"].fill_(P)
         s.meta["row_len"].fill_(P + 1)
         s.meta["row_start"].copy_(n_pads.to(torch.int32))
+
+    def _prefill_compute(self, s: Session, pre, B, P):
+        """The talker prefill forward over static buffers, then the first token (graph-capturable)."""
+        t, H = self.talker, self.talker.H
+        t.forward(pre["x"], B * P, pre["meta"], s.kv, pre["sc"], s.Lmax, P)
+        pre["last"].copy_(pre["x"].view(B, P, H)[:, -1])
+        K.rmsnorm(pre["last"], t.norm, t.eps, s.past_hidden, B, H)
+        K.gemm(s.past_hidden, self.codec_head, s.logits, B, H, self.V)
+        self._sample_talker(s, s.logits, 0, 99)
+
+    def _capture_prefill(self, s: Session, pre, B, P):
+        snap = s.ctr.clone(), s.seen.clone(), s.finished.clone(), s.codes.clone(), s.tok0.clone(), s.seed.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side), K.use_workspace(s.ws):
+            with torch.cuda.graph(g, stream=side):
+                self._prefill_compute(s, pre, B, P)
+        torch.cuda.current_stream().wait_stream(side)
+        s.ctr.copy_(snap[0]); s.seen.copy_(snap[1]); s.finished.copy_(snap[2]); s.codes.copy_(snap[3])
+        s.tok0.copy_(snap[4]); s.seed.copy_(snap[5])
+        return g
 
     def _capture(self, s: Session):
         # the graph must not see the prefill-time counter values: it only reads device memory

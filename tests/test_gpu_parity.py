@@ -894,6 +894,23 @@ def test_stream_chunk_schedule_grows(tiny_models):
     assert sizes[:5] == [1920 * 1, 1920 * 2, 1920 * 4, 1920 * 8, 1920 * 8], sizes
 
 
+def test_prefill_graph_replay_matches_eager(tiny_models):
+    """A repeated prompt length gets a captured talker prefill (second call captures, third replays): greedy codes
+    and hidden states of all three calls are identical, in fp32 and bf16."""
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    for dt in ("fp32", "bf16"):
+        model = TTSModel(cfg, W, dtype=dt)
+        case = dict(talker_cases()["cv_b3_auto_nospk"], max_new_tokens=12)
+        outs = [_run_case(model, "cv_b3_auto_nospk", case, 2, cfg) for _ in range(3)]
+        sess = model.engine.all_sessions()
+        assert any(pre["graph"] is not None for s in sess for pre in s.prefill.values())
+        for codes, hid in outs[1:]:
+            assert all(torch.equal(a, b) for a, b in zip(codes, outs[0][0]))
+            assert all(torch.equal(a, b) for a, b in zip(hid, outs[0][1]))
+
+
 def test_sampling_fresh_seed_per_call_reuses_session(tiny_models):
     """Sampling draws a fresh Philox key per generate() call (like the reference's torch.multinomial): two calls
     give different codes, torch.manual_seed reproduces a call, an explicit seed reproduces itself -- and every
