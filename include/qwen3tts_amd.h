@@ -73,7 +73,8 @@ typedef struct qt_gemm_args {
   /* QT_AACT_ELU: ELU(alpha = 1) on every A element (zero padding stays zero) -- the nn.ELU that precedes every
    * MimiConv1d of the tokenizer encoder (transformers modeling_mimi.py MimiEncoder / MimiResnetBlock) */
   int a_act;
-  /* optional bf16 copy of every element the epilogue stores (fp32 out, QT_EPI_STORE / QT_EPI_ADD, M <= 16):
+  /* optional bf16 copy of every element the epilogue stores (fp32 out, QT_EPI_STORE / QT_EPI_ADD; decode GEMV
+   * shapes: M <= 16, or the skinny row-group GEMV path of 17..96 rows / <= 256 rows of a <= 2048-column output):
    * out2[m*ldo2 + n] = bf16(out[m*ldo + n]).  Decode writes the residual stream this way so the next
    * RMS-normalised GEMV reads its A operand at half the bytes (its MFMA rounds A to bf16 anyway). */
   void* out2; long long ldo2;

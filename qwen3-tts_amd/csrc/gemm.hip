@@ -875,7 +875,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.gamma = a->gamma; p.eps = a->eps; p.rms = a->rmsnorm || a->gamma != nullptr; p.bias = a->bias; p.colscale = a->colscale;
   p.act = a->act; p.epi = a->epi; p.out = a->out; p.ldo = a->ldo;
   p.out2 = (bf16_t*)a->out2; p.ldo2 = a->ldo2;
-  if (p.out2 && (a->M > 16 || a->taps > 0 || a->epi == QT_EPI_SWIGLU || a->o_dtype != QT_F32)) return QT_ERR_ARG;
+  if (p.out2 && (a->taps > 0 || a->epi == QT_EPI_SWIGLU || a->o_dtype != QT_F32)) return QT_ERR_ARG;
   p.sn_a = a->snake_alpha; p.sn_ib = a->snake_inv_beta;
   if ((p.sn_a == nullptr) != (p.sn_ib == nullptr)) return QT_ERR_ARG;
   if (a->a_act != QT_AACT_NONE && a->a_act != QT_AACT_ELU) return QT_ERR_ARG;
@@ -929,7 +929,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
       // CP down 5.8 -> 5.6 us (o_proj / lm_head keep 16)
       if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
     }
-  } else if ((a->M <= 96 || (a->M <= gemv_max_m() && a->N <= 2048)) && a->taps == 0 && a->w_dtype == QT_BF16 &&
+  } else if (a->M <= gemv_max_m() && (a->M <= 96 || a->N <= 2048) && a->taps == 0 && a->w_dtype == QT_BF16 &&
              a->K % KT == 0 && a->gamma == nullptr && a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr) {
     // skinny GEMM (17..96 rows, or up to gemv_max_m rows of a <= 2048-column output: the talker prefill of
     // streaming-text prompts, short codec windows): the decode GEMV over row groups of 16 -- one block per (column
@@ -941,6 +941,8 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
     p.ks = 1;
     if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
   }
+  // out2 is written by the decode GEMV's epilogue only (M <= 16, or the skinny row-group path above)
+  if (p.out2 && (p.mr > 16 || a->K % KT != 0 || a->gamma != nullptr || a->a_act != QT_AACT_NONE)) return QT_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;
   if (w == QT_BF16 && ad == QT_F32 && o == QT_F32) return launch<bf16_t, float, float>(p, s);

@@ -75,8 +75,8 @@ class _Stack:
         and the next RMS GEMV (next layer's q/k/v, or the head W into out) as one persistent qt_cp_mlp launch."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
-        if x16 is not None and ("mlp_ws" in scratch or R > 16):
-            x16 = None  # the fused MLP / prefill GEMMs write x only
+        if x16 is not None and ("mlp_ws" in scratch or R > 96):
+            x16 = None  # the fused MLP / large-M prefill GEMMs write x only (decode / skinny GEMVs keep the shadow)
         xa = x if x16 is None else x16
         use_mlp = mlp is not None and fused_ao and x16 is not None and R <= 16
         for li, L in enumerate(self.layers):
@@ -471,7 +471,7 @@ class TalkerEngine:
             ln.x.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
             if ln.x16 is not None:
                 ln.x16.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
-        p16 = ln.x16 if 2 * nb <= 16 else None  # forward() keeps the shadow for decode-GEMV row counts only
+        p16 = ln.x16 if 2 * nb <= 96 else None  # forward() keeps the shadow for decode / skinny-GEMV row counts
         c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
         self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
         if ln.mlp is not None:
@@ -650,7 +650,10 @@ class TalkerEngine:
                             "row_len": torch.arange(1, P + 1, device=dev, dtype=torch.int32).repeat(B),
                             "row_start": i32(R),
                             "row_batch": torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(P)},
-                   "last": torch.empty(B, H, dtype=torch.float32, device=dev), "graph": None, "uses": 0}
+                   "last": torch.empty(B, H, dtype=torch.float32, device=dev), "graph": None, "uses": 0,
+                   # bf16 shadow of the prefill residual (skinny-GEMV row counts): the RMS GEMVs read half the bytes
+                   "x16": (torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+                           if X16 and self.wdt == torch.bfloat16 and R <= 96 else None)}
             s.prefill[P] = pre
         pre["meta"]["rope_pos"].copy_(pos.reshape(-1))
         pre["meta"]["row_start"].copy_(torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])
@@ -675,7 +678,9 @@ class TalkerEngine:
     def _prefill_compute(self, s: Session, pre, B, P):
         """The talker prefill forward over static buffers, then the first token (graph-capturable)."""
         t, H = self.talker, self.talker.H
-        t.forward(pre["x"], B * P, pre["meta"], s.kv, pre["sc"], s.Lmax, P)
+        if pre["x16"] is not None:
+            pre["x16"].copy_(pre["x"])
+        t.forward(pre["x"], B * P, pre["meta"], s.kv, pre["sc"], s.Lmax, P, x16=pre["x16"])
         pre["last"].copy_(pre["x"].view(B, P, H)[:, -1])
         K.rmsnorm(pre["last"], t.norm, t.eps, s.past_hidden, B, H)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, H, self.V)
