@@ -358,7 +358,8 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
 
 
 @pytest.mark.parametrize("D,hq,hkv,L,N,B", [(128, 16, 8, 17, 1024, 8), (128, 16, 8, 3, 1024, 16), (128, 8, 4, 40, 200, 3),
-                                            (16, 8, 2, 9, 32, 5), (64, 4, 4, 64, 96, 1), (128, 16, 4, 20, 256, 4)])
+                                            (16, 8, 2, 9, 32, 5), (64, 4, 4, 64, 96, 1), (128, 16, 4, 20, 256, 4),
+                                            (128, 16, 8, 16, 1024, 8), (128, 16, 8, 1, 1024, 3)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_decode_attn_oproj_matches_two_kernel_path(D, hq, hkv, L, N, B, dt):
     """qt_decode_attn_oproj (attention fused into o_proj + residual, head partials summed in-block) == qt_decode_attention

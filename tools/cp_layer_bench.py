@@ -12,7 +12,7 @@ dev = torch.device("cuda:0")
 
 
 def main():
-    B, H, hq, hkv, D, L = 8, 1024, 16, 8, 128, 17
+    B, H, hq, hkv, D, L = 8, 1024, 16, 8, 128, int(os.environ.get("QT_CPL_KEYS", "17"))
     dt = torch.bfloat16
     K.gemm_workspace(dev)
     nl = 5
