@@ -802,7 +802,8 @@ int launch(const GemmP& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_n1_k<AT, WT, OT>), dim3(batches * ((p.t_out + 255) / 256)), dim3(256), smem, s, p);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
-  } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 && p.M >= igemm_min_m() &&
+  } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 &&
+             p.M >= (p.taps > 0 ? 16 : igemm_min_m()) &&
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
     const int taps = p.taps == 0 ? 1 : p.taps, dil = p.taps == 0 ? 1 : p.dil;
     const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;
@@ -812,6 +813,14 @@ int launch(const GemmP& p, hipStream_t s) {
     // QT_IGEMM_G2 = 0 selects the 4 x 1 wave layout (measurement); default 2 x 2
     static const int g2 = [] { const char* e = getenv("QT_IGEMM_G2"); return e ? atoi(e) : 1; }();
     int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8, mi = 2;
+    // short windows (a streamed codec window, 1-3 frames x batch rows per conv): 64-row tiles and 4 (6) column
+    // tiles per block when the default tiling leaves fewer than 256 blocks -- the first streamed window's feed
+    // 2.53 -> 2.08 ms at B=8 (tools/codec_feed_prof.py)
+    if (!cfg) {
+      const int tout = p.taps == 0 ? p.M : p.t_out, nb = p.taps == 0 ? 1 : p.M / p.t_out;
+      const long long blocks = (long long)nb * ((tout + 127) / 128) * ((nt + ntb - 1) / ntb);
+      if (blocks < 256) { mi = 1; ntb = ntb == 6 ? 6 : 4; }
+    }
     if (cfg) { ntb = cfg / 10; mi = cfg % 10; }
     const int bm = 64 * mi;
     const int WR = bm + (taps - 1) * dil;

@@ -9,6 +9,7 @@ columns are already the time-interleaved samples: no pixel shuffle pass).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List
 
 import torch
@@ -104,6 +105,7 @@ class CodecDecoder:
         self.conv_last = K.tile_conv(g(f"decoder.decoder.{n + 2}.conv.weight"), g(f"decoder.decoder.{n + 2}.conv.bias"),
                                      wdt)
         self.total_upsample = int(math.prod(d["upsample_rates"]) * math.prod(d["upsampling_ratios"]))
+        self._slots = {}  # (B, max_frames) -> [_StreamSlot]: incremental-decode state reused across streams
         torch.cuda.synchronize()
 
     # ------------------------------------------------------------------------------------------------
@@ -203,8 +205,21 @@ class CodecDecoder:
         return pcm.view(B, L)
 
     def stream(self, B: int, max_frames: int) -> "CodecStream":
-        """A stateful incremental decode of up to max_frames frames (one reference chunk with its context)."""
+        """A stateful incremental decode of up to max_frames frames (one reference chunk with its context); close() it
+        to return its state slot (and the slot's captured feed graphs) to the pool."""
         return CodecStream(self, B, max_frames)
+
+    def _acquire_slot(self, B, max_frames) -> "_StreamSlot":
+        pool = self._slots.setdefault((B, max_frames), [])
+        for sl in pool:
+            if not sl.busy:
+                sl.reset()
+                sl.busy = True
+                return sl
+        sl = _StreamSlot(self, B, max_frames)
+        sl.busy = True
+        pool.append(sl)
+        return sl
 
     def chunked_decode(self, codes: torch.Tensor, chunk_size=300, left_context_size=25) -> torch.Tensor:
         """K:885-895 (codes [B, T, 16]; same chunk / left-context semantics, including the >300 quirks)."""
@@ -231,6 +246,31 @@ class CodecDecoder:
         return [a[:int(l)] for a, l in zip(wav, lengths)]
 
 
+class _StreamSlot:
+    """State of one incremental decode, reused by successive CodecStreams of the same (B, max_frames): the K/V caches,
+    every stage's input history (updated in place, so captured graphs keep pointing at it), the frame counter as a
+    device word, and the feed graphs captured on this slot keyed by (frames per feed, first feed)."""
+
+    def __init__(self, dec: "CodecDecoder", B: int, max_frames: int):
+        dev = dec.dev
+        self.kc = [torch.zeros(B, dec.kvh, max_frames, dec.hd, dtype=torch.float32, device=dev) for _ in dec.layers]
+        self.vc = [torch.zeros_like(k) for k in self.kc]
+        self.nf_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.hist = {}      # stage key -> [B][rows][C]
+        self.graphs = {}    # (n, first) -> (graph, static codes input, static pcm output)
+        self.uses = {}
+        self.busy = False
+
+    def reset(self):
+        for h in self.hist.values():
+            h.zero_()
+        self.nf_dev.zero_()
+
+
+# captured feed graphs (per slot and feed shape, once a shape repeats); QT_CODEC_GRAPH=0 always feeds eagerly (A/B)
+CODEC_GRAPH = os.environ.get("QT_CODEC_GRAPH", "1") == "1"
+
+
 class CodecStream:
     """Stateful incremental form of CodecDecoder.forward: frames are fed as they are generated and
     every output sample is computed once.  After n frames have been fed, samples [0, 1920 n - 555) of
@@ -240,31 +280,47 @@ class CodecStream:
     rows of every causal conv (zeros at the start = the one-shot zero padding), the last input row of every 2-tap
     transposed conv, the transformer's K/V caches (positions 0.. of this decode, window 72).  The per-row math is
     the one-shot's; only the GEMM row counts differ (results equal up to fp summation order).
+    A feed of ~140 small launches is host-bound, so a feed shape seen twice on a state slot is captured into a HIP
+    graph (positions come from the slot's device frame counter, histories are updated in place) and replayed.
+    close() hands the slot back to the decoder's pool.
     """
 
-    def __init__(self, dec: CodecDecoder, B: int, max_frames: int):
+    def __init__(self, dec: "CodecDecoder", B: int, max_frames: int):
         self.dec, self.B, self.max_frames = dec, B, max_frames
-        d, dev = dec.d, dec.dev
-        self.nf = 0  # frames fed
-        self.kc = [torch.zeros(B, dec.kvh, max_frames, dec.hd, dtype=torch.float32, device=dev) for _ in dec.layers]
-        self.vc = [torch.zeros_like(k) for k in self.kc]
+        d = dec.d
         if dec.cos.shape[0] < max_frames:
-            dec.cos, dec.sin = K.rope_tables(dec.hd, d["rope_theta"], max_frames + 64, dev)
-        self.hist = {}  # stage key -> [B][rows][C] input history
-        self.pcm = torch.zeros(B, dec.total_upsample * max_frames, dtype=torch.float32, device=dev)
+            dec.cos, dec.sin = K.rope_tables(dec.hd, d["rope_theta"], max_frames + 64, dec.dev)
+        self.slot = dec._acquire_slot(B, max_frames)
+        self.nf = 0  # frames fed
+        self.pcm = torch.zeros(B, dec.total_upsample * max_frames, dtype=torch.float32, device=dec.dev)
         self.ns = 0  # valid samples in self.pcm
 
+    def close(self):
+        if self.slot is not None:
+            self.slot.busy = False
+            self.slot = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     # -- stages ----------------------------------------------------------------------------------------
+    def _hist(self, key, rows, C, dtype):
+        h = self.slot.hist.get(key)
+        if h is None:  # first use on this slot (eager, never inside a capture): zeros = the one-shot zero padding
+            h = self.slot.hist[key] = torch.zeros(self.B, rows, C, dtype=dtype, device=self.dec.dev)
+        return h
+
     def _causal(self, key, x, n, Wt, cin, out=None, epi=_hip.EPI_STORE, snake=None):
         """x [B][n][cin] new input rows -> [B][n][Wt.N] outputs of the causal conv (history = previous inputs)."""
         dec, B = self.dec, self.B
         H = (Wt.taps - 1) * getattr(Wt, "dil", 1)
         if H:
-            h = self.hist.get(key)
-            if h is None:
-                h = torch.zeros(B, H, cin, dtype=x.dtype, device=x.device)
-            xin = torch.cat([h, x.view(B, n, cin)], 1).contiguous()
-            self.hist[key] = xin[:, -H:].clone()
+            h = self._hist(key, H, cin, x.dtype)
+            xin = torch.cat([h, x.view(B, n, cin)], 1)
+            h.copy_(xin[:, -H:])
         else:
             xin = x
         if out is None:
@@ -272,14 +328,14 @@ class CodecStream:
         dec._conv(xin, Wt, B, H + n, n, 0, out, cin, epi=epi, snake=snake)
         return out
 
-    def _tconv2(self, key, x, n, Wt, cin, snake):
+    def _tconv2(self, key, x, n, Wt, cin, snake, first):
         """2-tap transposed conv (row t <- inputs t, t + 1): returns (rows out, [B*rows][Wt.N])."""
         dec, B = self.dec, self.B
-        h = self.hist.get(key)
-        xin = x.view(B, n, cin) if h is None else torch.cat([h, x.view(B, n, cin)], 1)
+        h = self._hist(key, 1, cin, x.dtype)
+        xin = x.view(B, n, cin) if first else torch.cat([h, x.view(B, n, cin)], 1)
         xin = xin.contiguous()
         L = xin.shape[1]
-        self.hist[key] = xin[:, -1:].clone()
+        h.copy_(xin[:, -1:])
         rows = L - 1
         out = torch.empty(B * max(rows, 0), Wt.N, dtype=dec.adt, device=dec.dev)
         if rows > 0:
@@ -288,11 +344,12 @@ class CodecStream:
 
     def _transformer(self, h, n):
         dec, B, dev = self.dec, self.B, self.dec.dev
-        R, p0 = B * n, self.nf
+        R = B * n
         hid, nh, nkv, D = dec.hid, dec.heads, dec.kvh, dec.hd
         x = torch.empty(R, dec.inp.N, dtype=torch.float32, device=dev)
         K.gemm(h, dec.inp, x, R, dec.lat, dec.inp.N)
-        pos = torch.arange(p0, p0 + n, device=dev, dtype=torch.int32).repeat(B)
+        # positions nf .. nf + n - 1 from the slot's device frame counter (a captured feed replays with later ones)
+        pos = (torch.arange(n, device=dev, dtype=torch.int32) + self.slot.nf_dev).repeat(B)
         meta_b = torch.arange(B, device=dev, dtype=torch.int32).repeat_interleave(n)
         row_len, row_start = pos + 1, torch.zeros_like(pos)
         qkv_w = (nh + 2 * nkv) * D
@@ -302,10 +359,10 @@ class CodecStream:
         inter = dec.d["intermediate_size"]
         hmid = torch.empty(R, inter, dtype=torch.float32, device=dev)
         eps, win, Lm = dec.d["rms_norm_eps"], dec.d["sliding_window"], self.max_frames
-        for L, kc, vc in zip(dec.layers, self.kc, self.vc):
+        for L, kc, vc in zip(dec.layers, self.slot.kc, self.slot.vc):
             K.gemm(x, L["qkv"], qkv, R, hid, qkv_w, rms=True, eps=eps)
             K.qkv_post(qkv, R, nh, nkv, D, None, None, eps, dec.cos, dec.sin, pos, meta_b, pos, q, kc, vc, Lm)
-            K.attention(q, R, nh, nkv, D, kc, vc, Lm, meta_b, row_start, row_len, att, min(win, p0 + n), window=win)
+            K.attention(q, R, nh, nkv, D, kc, vc, Lm, meta_b, row_start, row_len, att, win, window=win)
             K.gemm(att, L["o"], x, R, nh * D, hid, colscale=L["ls1"], epi=_hip.EPI_ADD)
             K.gemm(x, L["gu"], hmid, R, hid, inter, rms=True, eps=eps, epi=_hip.EPI_SWIGLU)
             K.gemm(hmid, L["down"], x, R, inter, hid, colscale=L["ls2"], epi=_hip.EPI_ADD)
@@ -314,15 +371,10 @@ class CodecStream:
         return y
 
     # -- feeding ---------------------------------------------------------------------------------------
-    def feed(self, codes: torch.Tensor) -> int:
-        """codes int [B, n, 16] (the next n frames) -> number of valid samples now in self.pcm."""
+    def _compute(self, codes: torch.Tensor, n: int, first: bool):
+        """The device work of one feed (graph-capturable: no host-side state, fixed shapes for (n, first)); returns
+        the new clamped PCM rows [B][L]."""
         dec, B, dev, adt = self.dec, self.B, self.dec.dev, self.dec.adt
-        n = codes.shape[1]
-        if n == 0:
-            return self.ns
-        if self.nf + n > self.max_frames:
-            raise ValueError(f"CodecStream holds {self.max_frames} frames; {self.nf} fed, {n} more given")
-        codes = codes.to(dev, torch.int32).contiguous()
         # C1 (per frame)
         o1 = torch.empty(B * n, dec.cb_dim, dtype=torch.float32, device=dev)
         o2 = torch.empty_like(o1)
@@ -334,7 +386,7 @@ class CodecStream:
         # C2, C3
         x = self._causal("pre", h, n, dec.pre_conv, cd)
         x = self._transformer(x, n)
-        self.nf += n
+        self.slot.nf_dev.add_(n)
         # C4: upsample (1-tap transposed conv, no state) + ConvNeXt (causal depthwise k=7 + LayerNorm, then per row)
         L, C = n, dec.lat
         for i, u in enumerate(dec.ups):
@@ -343,12 +395,9 @@ class CodecStream:
             dec._conv(x, u["tconv"], B, L, L, 0, y, C)
             L *= f
             Hd = u["dw_w"].shape[1] - 1
-            hkey = f"dw{i}"
-            hst = self.hist.get(hkey)
-            if hst is None:
-                hst = torch.zeros(B, Hd, C, dtype=adt, device=dev)
-            yin = torch.cat([hst, y.view(B, L, C)], 1).contiguous()
-            self.hist[hkey] = yin[:, -Hd:].clone()
+            hst = self._hist(f"dw{i}", Hd, C, adt)
+            yin = torch.cat([hst, y.view(B, L, C)], 1)
+            hst.copy_(yin[:, -Hd:])
             z = torch.empty_like(yin)
             K.dwconv_ln(yin, B, Hd + L, C, u["dw_w"], u["dw_b"], u["ln_w"], u["ln_b"], 1e-6, z)
             z = z[:, Hd:].contiguous()
@@ -362,10 +411,10 @@ class CodecStream:
         # C6
         for bi, blk in enumerate(dec.blocks):
             r, cout = blk["r"], blk["cout"]
-            rows, y = self._tconv2(f"t{bi}", x, L, blk["tconv"], C, blk["s"])
+            rows, y = self._tconv2(f"t{bi}", x, L, blk["tconv"], C, blk["s"], first)
             L, C, x = rows * r, cout, y
             if L == 0:
-                return self.ns
+                return torch.zeros(B, 0, dtype=torch.float32, device=dev)
             for ui, un in enumerate(blk["units"]):
                 bb = self._causal(f"u{bi}.{ui}", x, L, un["c1"], C, snake=un["s1"])
                 self._causal(f"v{bi}.{ui}", bb, L, un["c2"], C, out=x, epi=_hip.EPI_ADD, snake=un["s2"])
@@ -374,6 +423,43 @@ class CodecStream:
                                                                             device=dev), snake=dec.s_last)
         pcm = out[:, 0].contiguous()
         K.clamp_pcm(pcm, pcm.numel(), pcm)
-        self.pcm[:, self.ns:self.ns + L] = pcm.view(B, L)
+        return pcm.view(B, L)
+
+    def feed(self, codes: torch.Tensor) -> int:
+        """codes int [B, n, 16] (the next n frames) -> number of valid samples now in self.pcm."""
+        dec, B, dev = self.dec, self.B, self.dec.dev
+        n = codes.shape[1]
+        if n == 0:
+            return self.ns
+        if self.nf + n > self.max_frames:
+            raise ValueError(f"CodecStream holds {self.max_frames} frames; {self.nf} fed, {n} more given")
+        codes = codes.to(dev, torch.int32).contiguous()
+        key = (n, self.nf == 0)
+        slot = self.slot
+        g = slot.graphs.get(key)
+        if g is not None:
+            g[1].copy_(codes)
+            g[0].replay()
+            pcm = g[2]
+        else:
+            pcm = self._compute(codes, n, key[1])
+            slot.uses[key] = slot.uses.get(key, 0) + 1
+            if CODEC_GRAPH and slot.uses[key] >= 2:
+                slot.graphs[key] = self._capture(codes, n, key[1])
+        self.nf += n
+        L = pcm.shape[1]
+        self.pcm[:, self.ns:self.ns + L] = pcm
         self.ns += L
         return self.ns
+
+    def _capture(self, codes, n, first):
+        # capturing executes nothing: the slot state (histories, caches, frame counter) is left as the eager feed left it
+        cin = codes.clone()
+        side = torch.cuda.Stream(device=self.dec.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dec.dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                out = self._compute(cin, n, first)
+        torch.cuda.current_stream(self.dec.dev).wait_stream(side)
+        return g, cin, out

@@ -265,61 +265,67 @@ class TTSModel:
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames + 1, grow=True)
         cs, cs_k, cs_fed = None, -1, 0    # stateful decoder of reference chunk cs_k, fed frames [.., cs_fed)
-        for sessions, frames, final in it:
-            # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
-            codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
-            c0 = codes[:, :, 0].cpu()
-            for b in range(B):
-                if end[b] is None:
-                    hit = (c0[b, emitted:] == eos).nonzero()
-                    if hit.numel():
-                        end[b] = emitted + int(hit[0])
-                if final and end[b] is None:
-                    end[b] = frames
-                if end[b] is not None and cap[b] is None:
-                    cap[b] = up * int((c0[b, :end[b]] != 0).sum())
-            # the batch's length once known: every row ended (longest row), or generation stopped
-            t_end = max(end) if all(x is not None for x in end) else None
-            target = t_end if t_end is not None else frames - 1  # else keep frame `frames-1` as lookahead
-            while emitted < target:
-                k = emitted // RC
-                cend = (k + 1) * RC
-                e = min(target, cend)
-                closed = e == cend or e == t_end  # this reference chunk ends at e
-                base = k * RC - (RX if k * RC - RX > 0 else k * RC)
-                hi = e if closed else e + 1
-                if left_context is None:
-                    if cs_k != k:  # a new reference chunk: a fresh decoder, primed from the chunk's context frames
-                        cs, cs_k, cs_fed = dec.stream(B, RX + RC), k, base
-                    lo, ctx = cs_fed, emitted - base
-                else:
-                    ctx = min(emitted - base, left_context)
-                    lo = emitted - ctx
-                cc = codes[:, lo:hi].clone()
-                for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
-                    if end[b] is not None and end[b] < hi:
-                        cc[b, max(end[b] - lo, 0):] = 0
-                if left_context is None:
-                    cs.feed(cc)
-                    cs_fed = hi
-                    w = cs.pcm
-                else:
-                    w = dec.forward(cc)
-                n = up * (e - emitted) - (555 if closed else 0)
+        try:
+            for sessions, frames, final in it:
+                # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
+                codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
+                c0 = codes[:, :, 0].cpu()
                 for b in range(B):
-                    if done[b]:
-                        continue
-                    take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
-                    chunk = w[b, ctx * up:ctx * up + take]
-                    cum[b] += take
-                    last = cap[b] is not None and (cum[b] >= cap[b] or e == t_end)
-                    done[b] = last
-                    yield b, chunk, last
-                emitted = e
-            if t_end is not None and emitted >= t_end:
-                for b in range(B):  # rows whose output was complete before the last window
-                    if not done[b]:
-                        done[b] = True
-                        yield b, torch.zeros(0, device=codes.device), True
-            if all(done):
-                break
+                    if end[b] is None:
+                        hit = (c0[b, emitted:] == eos).nonzero()
+                        if hit.numel():
+                            end[b] = emitted + int(hit[0])
+                    if final and end[b] is None:
+                        end[b] = frames
+                    if end[b] is not None and cap[b] is None:
+                        cap[b] = up * int((c0[b, :end[b]] != 0).sum())
+                # the batch's length once known: every row ended (longest row), or generation stopped
+                t_end = max(end) if all(x is not None for x in end) else None
+                target = t_end if t_end is not None else frames - 1  # else keep frame `frames-1` as lookahead
+                while emitted < target:
+                    k = emitted // RC
+                    cend = (k + 1) * RC
+                    e = min(target, cend)
+                    closed = e == cend or e == t_end  # this reference chunk ends at e
+                    base = k * RC - (RX if k * RC - RX > 0 else k * RC)
+                    hi = e if closed else e + 1
+                    if left_context is None:
+                        if cs_k != k:  # a new reference chunk: a fresh decoder, primed from the chunk's context frames
+                            if cs is not None:
+                                cs.close()
+                            cs, cs_k, cs_fed = dec.stream(B, RX + RC), k, base
+                        lo, ctx = cs_fed, emitted - base
+                    else:
+                        ctx = min(emitted - base, left_context)
+                        lo = emitted - ctx
+                    cc = codes[:, lo:hi].clone()
+                    for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
+                        if end[b] is not None and end[b] < hi:
+                            cc[b, max(end[b] - lo, 0):] = 0
+                    if left_context is None:
+                        cs.feed(cc)
+                        cs_fed = hi
+                        w = cs.pcm
+                    else:
+                        w = dec.forward(cc)
+                    n = up * (e - emitted) - (555 if closed else 0)
+                    for b in range(B):
+                        if done[b]:
+                            continue
+                        take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
+                        chunk = w[b, ctx * up:ctx * up + take]
+                        cum[b] += take
+                        last = cap[b] is not None and (cum[b] >= cap[b] or e == t_end)
+                        done[b] = last
+                        yield b, chunk, last
+                    emitted = e
+                if t_end is not None and emitted >= t_end:
+                    for b in range(B):  # rows whose output was complete before the last window
+                        if not done[b]:
+                            done[b] = True
+                            yield b, torch.zeros(0, device=codes.device), True
+                if all(done):
+                    break
+        finally:
+            if cs is not None:
+                cs.close()

@@ -1041,21 +1041,30 @@ def test_codec_stream_matches_forward(preset, dtype):
     codes = torch.randint(1, dec.tables.shape[1], (B, T, dec.tables.shape[0]), generator=g).to(dev, torch.int32)
     codes[1, 70:] = 0  # a row that ended early: zero padding, as in a ragged batch decode
     ref = dec.forward(codes)
-    cs = dec.stream(B, T)
-    fed = 0
-    for n in (1, 3, 1, 8, 40, 37):
-        ns = cs.feed(codes[:, fed:fed + n])
-        fed += n
-        assert ns == 1920 * fed - 555
-        got, exp = cs.pcm[:, :ns], ref[:, :ns]
-        if dtype == "fp32":
-            torch.testing.assert_close(got, exp, atol=2e-5, rtol=0)
-        else:
-            rel = float((got - exp).norm() / exp.norm())
-            assert rel < 2e-2, (fed, rel)
-    assert fed == T
-    with pytest.raises(ValueError):
-        cs.feed(codes[:, :1])
+    # three streams in a row on the decoder's pooled state slot: the first feeds eagerly, the second captures each
+    # feed shape into a graph, the third replays them -- all three equal forward()
+    pcms = []
+    for rep in range(3):
+        cs = dec.stream(B, T)
+        fed = 0
+        for n in (1, 3, 1, 8, 40, 37):
+            ns = cs.feed(codes[:, fed:fed + n])
+            fed += n
+            assert ns == 1920 * fed - 555
+            got, exp = cs.pcm[:, :ns], ref[:, :ns]
+            if dtype == "fp32":
+                torch.testing.assert_close(got, exp, atol=2e-5, rtol=0)
+            else:
+                rel = float((got - exp).norm() / exp.norm())
+                assert rel < 2e-2, (fed, rel)
+        assert fed == T
+        with pytest.raises(ValueError):
+            cs.feed(codes[:, :1])
+        pcms.append(cs.pcm[:, :ns].clone())
+        if rep == 2:
+            assert len(cs.slot.graphs) == 6
+        cs.close()
+    assert torch.equal(pcms[1], pcms[2])  # captured replay == the eager feed it was captured from
 
 
 @pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice")])
