@@ -338,9 +338,8 @@ class Qwen3TTSModel:
                first_chunk_frames=2, chunk_frames=48, left_context=None, **kwargs):
         """New surface (no reference counterpart): streaming custom-voice generation.
         Yields (utterance index, pcm chunk np.float32, sample rate, is_last) while the batch decodes: the first
-        chunk covers `first_chunk_frames` frames (2 frames = 0.16 s of audio: the first packet arrives after prefill +
-        3 decode frames), later chunks double in size up to `chunk_frames` (each chunk's audio outlasts the
-        generation of the next).  Per utterance the
+        chunk arrives after prefill + `first_chunk_frames` decode frames (2 frames: 3285 samples = 0.14 s of audio),
+        later chunks double in size up to `chunk_frames` (each chunk's audio outlasts the generation of the next).  Per utterance the
         chunks concatenate to the one-shot generate_custom_voice() length and equal its PCM up to fp summation order
         (a stateful incremental codec decode; codes are identical -- see TTSModel.stream for the chunk rule and the
         stateless `left_context` form)."""

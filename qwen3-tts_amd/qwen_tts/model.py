@@ -238,11 +238,12 @@ class TTSModel:
 
         Per row the chunks concatenate to the one-shot generate() + decode() PCM (Z:259-365): the reference
         decodes the zero-right-padded batch in 300-frame chunks with 25 frames of left context, dropping the
-        last 555 samples of each chunk (no next frame), and keeps 1920 x #nonzero-cb0 samples.  A streamed
-        window [s, e) never crosses a chunk boundary and needs one lookahead frame.  Default (left_context=None):
-        one stateful incremental decoder per reference chunk (codec.CodecStream, primed with the chunk's 25 context
-        frames) is fed each frame once, so every sample is computed once and equals the one-shot output up to fp
-        summation order.  An int `left_context` selects the stateless form instead: each window is re-decoded from
+        last 555 samples of each chunk (no next frame), and keeps 1920 x #nonzero-cb0 samples.  Default
+        (left_context=None): one stateful incremental decoder per reference chunk (codec.CodecStream, primed with the
+        chunk's 25 context frames) is fed each final frame once and every sample computable so far is emitted (a
+        chunk yields 1920 n - 555 samples after its n frames: no lookahead frame is waited for), so every sample is
+        computed once and equals the one-shot output up to fp summation order.  An int `left_context` selects the
+        stateless form instead (windows [s, e) within a reference chunk, one lookahead frame), re-decoded from
         min(its chunk's start, left_context frames back) -- 325 reproduces the reference, less is approximate (in
         fp32 150 frames -> rel-L2 1e-6, 72 -> 7e-4, 25 -> 2e-2; tools/stream_fidelity.py).  Codes are identical to
         generate().  pcm is a 1-D fp32 device tensor of 24 kHz samples."""
@@ -262,9 +263,76 @@ class TTSModel:
         cum = [0] * B                     # samples emitted per row
         # chunk sizes double from first_chunk_frames up to chunk_frames: each chunk's audio (80 ms per frame) covers
         # the generation of the next one (~3 ms per frame), so playback started at the first packet never starves
+        if left_context is None:
+            yield from self._stream_stateful(dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames,
+                                             use_graph)
+            return
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames + 1, grow=True)
-        cs, cs_k, cs_fed = None, -1, 0    # stateful decoder of reference chunk cs_k, fed frames [.., cs_fed)
+        for sessions, frames, final in it:
+            # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
+            codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
+            c0 = codes[:, :, 0].cpu()
+            for b in range(B):
+                if end[b] is None:
+                    hit = (c0[b, emitted:] == eos).nonzero()
+                    if hit.numel():
+                        end[b] = emitted + int(hit[0])
+                if final and end[b] is None:
+                    end[b] = frames
+                if end[b] is not None and cap[b] is None:
+                    cap[b] = up * int((c0[b, :end[b]] != 0).sum())
+            # the batch's length once known: every row ended (longest row), or generation stopped
+            t_end = max(end) if all(x is not None for x in end) else None
+            target = t_end if t_end is not None else frames - 1  # else keep frame `frames-1` as lookahead
+            while emitted < target:
+                k = emitted // RC
+                cend = (k + 1) * RC
+                e = min(target, cend)
+                closed = e == cend or e == t_end  # this reference chunk ends at e
+                base = k * RC - (RX if k * RC - RX > 0 else k * RC)
+                hi = e if closed else e + 1
+                ctx = min(emitted - base, left_context)
+                lo = emitted - ctx
+                cc = codes[:, lo:hi].clone()
+                for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
+                    if end[b] is not None and end[b] < hi:
+                        cc[b, max(end[b] - lo, 0):] = 0
+                w = dec.forward(cc)
+                n = up * (e - emitted) - (555 if closed else 0)
+                for b in range(B):
+                    if done[b]:
+                        continue
+                    take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
+                    chunk = w[b, ctx * up:ctx * up + take]
+                    cum[b] += take
+                    last = cap[b] is not None and (cum[b] >= cap[b] or e == t_end)
+                    done[b] = last
+                    yield b, chunk, last
+                emitted = e
+            if t_end is not None and emitted >= t_end:
+                for b in range(B):  # rows whose output was complete before the last window
+                    if not done[b]:
+                        done[b] = True
+                        yield b, torch.zeros(0, device=codes.device), True
+            if all(done):
+                break
+
+    def _stream_stateful(self, dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames, use_graph):
+        """stream() on the incremental codec: every final frame is fed once to the decoder of its reference chunk
+        and every sample computable from the frames fed so far is emitted -- 1920 n - 555 samples of a chunk after
+        its n frames, i.e. no lookahead frame is waited for (the 555 samples that need it follow with the next
+        chunk; at a reference chunk's end they are dropped, as the reference's chunked decode drops them)."""
+        up = dec.total_upsample
+        RC, RX = self.REF_CHUNK, self.REF_CTX
+        end = [None] * B                  # frame count of each row once its EOS is seen
+        cap = [None] * B                  # one-shot sample count (1920 x #nonzero cb0) once the row has ended
+        done = [False] * B
+        cum = [0] * B                     # samples emitted per row
+        scanned = 0                       # cb0 columns already searched for EOS
+        k, cs, fed, emit_s, ctx_s = 0, None, 0, 0, 0   # reference chunk, its decoder, frames fed, samples emitted
+        it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
+                                     first=first_chunk_frames, grow=True)
         try:
             for sessions, frames, final in it:
                 # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
@@ -272,54 +340,47 @@ class TTSModel:
                 c0 = codes[:, :, 0].cpu()
                 for b in range(B):
                     if end[b] is None:
-                        hit = (c0[b, emitted:] == eos).nonzero()
+                        hit = (c0[b, scanned:] == eos).nonzero()
                         if hit.numel():
-                            end[b] = emitted + int(hit[0])
+                            end[b] = scanned + int(hit[0])
                     if final and end[b] is None:
                         end[b] = frames
                     if end[b] is not None and cap[b] is None:
                         cap[b] = up * int((c0[b, :end[b]] != 0).sum())
-                # the batch's length once known: every row ended (longest row), or generation stopped
+                scanned = frames
                 t_end = max(end) if all(x is not None for x in end) else None
-                target = t_end if t_end is not None else frames - 1  # else keep frame `frames-1` as lookahead
-                while emitted < target:
-                    k = emitted // RC
+                avail = t_end if t_end is not None else frames
+                while True:
                     cend = (k + 1) * RC
-                    e = min(target, cend)
-                    closed = e == cend or e == t_end  # this reference chunk ends at e
-                    base = k * RC - (RX if k * RC - RX > 0 else k * RC)
-                    hi = e if closed else e + 1
-                    if left_context is None:
-                        if cs_k != k:  # a new reference chunk: a fresh decoder, primed from the chunk's context frames
-                            if cs is not None:
-                                cs.close()
-                            cs, cs_k, cs_fed = dec.stream(B, RX + RC), k, base
-                        lo, ctx = cs_fed, emitted - base
-                    else:
-                        ctx = min(emitted - base, left_context)
-                        lo = emitted - ctx
-                    cc = codes[:, lo:hi].clone()
-                    for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
-                        if end[b] is not None and end[b] < hi:
-                            cc[b, max(end[b] - lo, 0):] = 0
-                    if left_context is None:
+                    if cs is None:  # reference chunk k: a fresh decoder, primed from its 25 context frames
+                        base = k * RC - (RX if k * RC - RX > 0 else k * RC)
+                        cs, fed, emit_s, ctx_s = dec.stream(B, RX + RC), base, 0, (k * RC - base) * up
+                    hi = min(avail, cend)
+                    if hi > fed:
+                        cc = codes[:, fed:hi].clone()
+                        for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
+                            if end[b] is not None and end[b] < hi:
+                                cc[b, max(end[b] - fed, 0):] = 0
                         cs.feed(cc)
-                        cs_fed = hi
-                        w = cs.pcm
-                    else:
-                        w = dec.forward(cc)
-                    n = up * (e - emitted) - (555 if closed else 0)
+                        fed = hi
+                    n = max(cs.ns - ctx_s - emit_s, 0)
+                    ended = t_end is not None and fed >= t_end
                     for b in range(B):
-                        if done[b]:
+                        if done[b] or n == 0:
                             continue
                         take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
-                        chunk = w[b, ctx * up:ctx * up + take]
+                        chunk = cs.pcm[b, ctx_s + emit_s:ctx_s + emit_s + take]
                         cum[b] += take
-                        last = cap[b] is not None and (cum[b] >= cap[b] or e == t_end)
+                        last = cap[b] is not None and (cum[b] >= cap[b] or ended)
                         done[b] = last
                         yield b, chunk, last
-                    emitted = e
-                if t_end is not None and emitted >= t_end:
+                    emit_s += n
+                    if fed == cend and not ended:  # chunk k complete (its 555-sample tail is dropped): next chunk
+                        cs.close()
+                        cs, k = None, k + 1
+                        continue
+                    break
+                if t_end is not None and fed >= t_end:
                     for b in range(B):  # rows whose output was complete before the last window
                         if not done[b]:
                             done[b] = True

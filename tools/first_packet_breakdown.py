@@ -1,6 +1,6 @@
 """Where the first packet's time goes at the bench configuration (1.7B synthetic, B=8 and B=1, 200-token prompts,
 streaming text): prompt assembly, prefill + first frame (generate with max_new_tokens=1), each further frame, and
-the codec's first incremental feed (first_chunk_frames + 1 = 3 frames)."""
+the codec's first incremental feed (first_chunk_frames = 2 frames)."""
 import os
 import sys
 import time
@@ -39,7 +39,7 @@ def main():
         t_prompt = timed(lambda: m.build_prompts(ids, ["english"] * B, spk[:B], None, False, None, None))
         t1 = timed(lambda: m.generate(max_new_tokens=1, **kw, **gen))
         t6 = timed(lambda: m.generate(max_new_tokens=6, **kw, **gen))
-        codes = torch.randint(1, 2048, (B, 3, 16), device=dev, dtype=torch.int32)
+        codes = torch.randint(1, 2048, (B, 2, 16), device=dev, dtype=torch.int32)
         dec = m.speech_tokenizer.model
 
         def feed():
@@ -51,7 +51,7 @@ def main():
                 break
         t_fp = timed(first)
         print(f"B={B}: prompt assembly {t_prompt:.1f} ms | generate(1 frame) {t1:.1f} | generate(6) {t6:.1f} "
-              f"(+{(t6 - t1) / 5:.2f} per frame) | codec feed of 3 frames {t_codec:.1f} | stream first packet {t_fp:.1f}",
+              f"(+{(t6 - t1) / 5:.2f} per frame) | codec feed of 2 frames {t_codec:.1f} | stream first packet {t_fp:.1f}",
               flush=True)
 
 
