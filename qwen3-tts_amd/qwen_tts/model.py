@@ -34,7 +34,7 @@ class _Runs:
 
     def run(self, e):
         if self.ids["t"]:
-            self.out["t"] = e.text_proj(torch.tensor(self.ids["t"], dtype=torch.int32))
+            self.out["t"] = e.text_proj(self.ids["t"])
         if self.ids["c"]:
             self.out["c"] = e.codec_embed(self.ids["c"])
 

@@ -20,6 +20,17 @@ from . import _hip
 from . import kernels as K
 
 
+def _to_dev_i32(ids, dev) -> torch.Tensor:
+    """Token ids (list / host tensor / device tensor) as a flat device int32 tensor. Host ids go through pinned
+    memory with a non-blocking copy: a pageable upload waits for all queued GPU work."""
+    if isinstance(ids, torch.Tensor) and ids.device.type != "cpu":
+        return ids.reshape(-1).to(dev, torch.int32)
+    h = torch.as_tensor(ids, dtype=torch.int32).reshape(-1)
+    if dev.type != "cuda":
+        return h.to(dev)
+    return h.pin_memory().to(dev, non_blocking=True)
+
+
 def _w(W, name, dev):
     t = W[name]
     if not isinstance(t, torch.Tensor):
@@ -348,7 +359,7 @@ class TalkerEngine:
     # ---------------------------------------------------------------- G1: prompt embeddings
     def text_proj(self, ids: torch.Tensor) -> torch.Tensor:
         """text_projection(text_embedding(ids)) (M:808-816): gather -> fc1(+b, SiLU) -> fc2(+b); fp32 [n, H]."""
-        ids = ids.reshape(-1).to(self.dev, torch.int32)
+        ids = _to_dev_i32(ids, self.dev)
         n = ids.numel()
         thd = self.text_emb.shape[1]
         h = torch.empty(n, self.fc1.N, dtype=torch.float32, device=self.dev)
@@ -359,14 +370,14 @@ class TalkerEngine:
         return out
 
     def codec_embed(self, ids) -> torch.Tensor:
-        ids = torch.as_tensor(ids, dtype=torch.int32, device=self.dev).reshape(-1)
+        ids = _to_dev_i32(ids, self.dev)
         H = self.talker.H
         out = torch.empty(ids.numel(), H, dtype=torch.float32, device=self.dev)
         K.gather_rows(self.emb0, ids, ids.numel(), H, out, H)
         return out
 
     def cp_embed(self, g, ids) -> torch.Tensor:
-        ids = torch.as_tensor(ids, dtype=torch.int32, device=self.dev).reshape(-1)
+        ids = _to_dev_i32(ids, self.dev)
         H = self.talker.H
         out = torch.empty(ids.numel(), H, dtype=torch.float32, device=self.dev)
         K.gather_rows(self.ecp[g], ids, ids.numel(), H, out, H)
@@ -669,7 +680,7 @@ class TalkerEngine:
             if PREFILL_GRAPH and pre["uses"] >= 2:
                 pre["graph"] = self._capture_prefill(s, pre, B, P)
         # decode counters: step 0, one token generated, pos = P + delta, kv_pos = P, len = P + 1
-        s.ctr[1] = 1
+        s.ctr[1:2].fill_(1)  # a device fill: item assignment uploads a host scalar and waits for the prefill
         s.meta["rope_pos"].copy_((P + rope_delta).to(torch.int32))
         s.meta["kv_pos"].fill_(P)
         s.meta["row_len"].fill_(P + 1)

@@ -1,5 +1,6 @@
 """Kernel mix of one incremental codec feed (the stream's first window: 3 frames) at the 1.7B dims, B=8, replayed
-from its captured graph -- run under rocprofv3 --kernel-trace (tools/prof_codec_feed.sh)."""
+from its captured graph -- run under rocprofv3 --kernel-trace. QT_CF_N frames (default 2 = the stream's first
+packet since it emits without a lookahead frame), QT_CF_B rows."""
 import os
 import sys
 import torch
@@ -16,7 +17,8 @@ def main():
     ccfg = read_json(os.path.join(d, "speech_tokenizer", "config.json"))
     dec = CodecDecoder(ccfg, synthetic(codec_specs(ccfg), dev), dtype="bf16", device=str(dev))
     B = int(os.environ.get("QT_CF_B", "8"))
-    codes = torch.randint(1, 2048, (B, 3, 16), device=dev, dtype=torch.int32)
+    n = int(os.environ.get("QT_CF_N", "2"))
+    codes = torch.randint(1, 2048, (B, n, 16), device=dev, dtype=torch.int32)
     for _ in range(20):
         cs = dec.stream(B, 325)
         cs.feed(codes)
@@ -33,7 +35,7 @@ def main():
         ts.append((time.perf_counter() - t0) * 1e3)
         cs.close()
     ts.sort()
-    print(f"B={B} first-window feed (3 frames, replayed graph): {ts[5]:.3f} ms", flush=True)
+    print(f"B={B} first-window feed ({n} frames, replayed graph): {ts[5]:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
