@@ -250,28 +250,38 @@ typedef struct qt_sample_args {
   const float* emb2_table; int emb2_dim; float* emb2_out; long long emb2_ld;
   int algo;  /* top-k (<= 64) sampling path, tests / measurement: 0 auto (histogram, per-wave on fall-through),
               * 1 per-wave candidate lists only, 2 histogram (same as 0).  Same Philox draws, same tokens. */
+  /* per-row counters (continuous batching, every row its own request): row r reads step[r * ctr_stride] and
+   * n_generated[r * ctr_stride]; 0 = one counter shared by every row */
+  int ctr_stride;
+  /* optional per-row Philox stream id (NULL -> row_base + r): a request keeps the stream of its index in the
+   * request list whichever batch slot decodes it */
+  const int* philox_row;
 } qt_sample_args;
 int qt_sample(const qt_sample_args* args, void* stream);
 
 /* Qwen3TTSRMSNorm (M:595-610 / K:372-390): out = gamma * (x * rsqrt(mean(x^2) + eps)), fp32 [M][N]. */
 int qt_rmsnorm(const float* x, const float* gamma, float eps, float* out, int M, int N, void* stream);
-/* qt_rmsnorm + a record of each normalised row at rec[m*rec_ld + (*step + step_off)*N] (per-frame hidden states
- * written inside the captured frame graph at the device step counter). */
+/* qt_rmsnorm + a record of each normalised row at rec[m*rec_ld + (step[m*step_stride] + step_off)*N] (per-frame
+ * hidden states written inside the captured frame graph at the device step counter(s)). */
 int qt_rmsnorm_rec(const float* x, const float* gamma, float eps, float* out, int M, int N, float* rec,
-                   long long rec_ld, const int* step, int step_off, void* stream);
+                   long long rec_ld, const int* step, int step_off, int step_stride, void* stream);
 
 /* out[m] = table[idx[m]] (fp32 out, table dtype), nn.Embedding row gather (M:1441, 1670). */
 int qt_gather_rows(const void* table, int dtype, const int* idx, int M, int H, float* out, long long ldo, void* stream);
 
 /* Talker decode input (M:1681-1692): x[b] = E0[codes[b,t,0]] + sum_g Ecp[g][codes[b,t,1+g]]
- * + (t < T ? trailing[b][t] : pad).  codes: int32 [B][codes_ld] rows holding [F][G].  x16 (optional):
- * bf16 copy of x ([B][H]), the A operand of the first layer's RMS-normalised QKV GEMV. */
+ * + (t < T ? trailing[b][t] : pad), t = step[b*step_stride].  codes: int32 [B][codes_ld] rows holding [F][G].
+ * x16 (optional): bf16 copy of x ([B][H]), the A operand of the first layer's RMS-normalised QKV GEMV. */
 int qt_frame_embed(const void* emb0, const void* emb_cp, int dtype, int V0, int Vcp, int G, int H,
-                   const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
-                   const float* pad, float* x, void* x16, int B, void* stream);
+                   const int* codes, long long codes_ld, const int* step, int step_stride, const float* trailing,
+                   int T, const float* pad, float* x, void* x16, int B, void* stream);
 
 /* counters[i] += 1 for i < n (end-of-frame step / position advance inside a captured graph). */
 int qt_advance(int* counters, int n, void* stream);
+/* per-row counters, field-major [nfields][B], field 0 = each row's frame index: row b advances every field by one
+ * while counters[b] < cap (a finished batch slot awaiting its next request stays at frame cap).  The end-of-frame
+ * advance of the replaced loop's `cache_position` / `rope_deltas` bookkeeping (M:1693-1711), per request. */
+int qt_advance_rows(int* counters, int B, int nfields, int cap, void* stream);
 
 /* ---- codec decoder helpers (K) ---- */
 /* SplitResidualVectorQuantizer.decode table gather-sum (K:814-820): out[b][t][:] = sum_q tab_q[codes[b][t][q]],

@@ -8,7 +8,7 @@ namespace {
 __global__ __launch_bounds__(256) void rmsnorm_k(const float* __restrict__ x, const float* __restrict__ g, float eps,
                                                  float* __restrict__ out, int N, float* __restrict__ rec = nullptr,
                                                  long long rec_ld = 0, const int* __restrict__ step = nullptr,
-                                                 int step_off = 0) {
+                                                 int step_off = 0, int step_stride = 0) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   const float* xr = x + (long long)m * N;
@@ -18,7 +18,7 @@ __global__ __launch_bounds__(256) void rmsnorm_k(const float* __restrict__ x, co
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
   const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
-  float* rr = rec ? rec + (long long)m * rec_ld + (long long)(*step + step_off) * N : nullptr;
+  float* rr = rec ? rec + (long long)m * rec_ld + (long long)(step[m * step_stride] + step_off) * N : nullptr;
   for (int i = tid; i < N; i += 256) {
     const float v = g[i] * (xr[i] * rs);
     out[(long long)m * N + i] = v;
@@ -38,7 +38,7 @@ template <typename ET>
 __global__ __launch_bounds__(64) void frame_embed_k(const ET* __restrict__ e0, const ET* __restrict__ ecp, int V0,
                                                      int Vcp, int G, int H, const int* __restrict__ codes,
                                                      long long codes_ld, const int* __restrict__ step,
-                                                     const float* __restrict__ trailing, int T,
+                                                     int step_stride, const float* __restrict__ trailing, int T,
                                                      const float* __restrict__ pad, float* __restrict__ x,
                                                      bf16_t* __restrict__ x16) {
   // ET: table dtype.  Block (b, y) sums dims [y * 8 * blockDim, ...) of row b (several blocks per row: the 16
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(64) void frame_embed_k(const ET* __restrict__ e0, c
   // then every thread issues its 16 row-slice loads before summing.
   __shared__ int cs[32];
   const int b = blockIdx.x;
-  const int t = *step;
+  const int t = step[b * step_stride];  // per-row frame index (step_stride 1) or one shared counter (0)
   if (threadIdx.x < G) cs[threadIdx.x] = codes[(long long)b * codes_ld + (long long)t * G + threadIdx.x];
   __syncthreads();
   const float* tr = t < T ? trailing + ((long long)b * T + t) * H : pad;
@@ -72,6 +72,15 @@ __global__ __launch_bounds__(64) void frame_embed_k(const ET* __restrict__ e0, c
 __global__ void advance_k(int* c, int n) {
   int i = threadIdx.x;
   if (i < n) c[i] += 1;
+}
+
+// per-row counters, field-major [nf][B] with field 0 = the row's frame index: a row advances all its fields
+// together until its frame index reaches cap, then stays (a finished slot waiting to be refilled keeps re-running
+// frame `cap` in place instead of writing past its buffers)
+__global__ void advance_rows_k(int* c, int B, int nf, int cap) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || c[b] >= cap) return;
+  for (int f = 0; f < nf; ++f) c[f * B + b] += 1;
 }
 
 __global__ void rvq_gather_k(const float* __restrict__ tabs, int Q, int n_first, int cb, int dim,
@@ -162,9 +171,10 @@ extern "C" int qt_rmsnorm(const float* x, const float* g, float eps, float* out,
 }
 
 extern "C" int qt_rmsnorm_rec(const float* x, const float* g, float eps, float* out, int M, int N, float* rec,
-                              long long rec_ld, const int* step, int step_off, void* s) {
-  if (M <= 0 || N <= 0 || !rec || !step) return QT_ERR_SHAPE;
-  hipLaunchKernelGGL(rmsnorm_k, dim3(M), dim3(256), 0, (hipStream_t)s, x, g, eps, out, N, rec, rec_ld, step, step_off);
+                              long long rec_ld, const int* step, int step_off, int step_stride, void* s) {
+  if (M <= 0 || N <= 0 || !rec || !step || step_stride < 0) return QT_ERR_SHAPE;
+  hipLaunchKernelGGL(rmsnorm_k, dim3(M), dim3(256), 0, (hipStream_t)s, x, g, eps, out, N, rec, rec_ld, step, step_off,
+                     step_stride);
   return ok();
 }
 
@@ -181,16 +191,16 @@ extern "C" int qt_gather_rows(const void* tab, int dtype, const int* idx, int M,
 }
 
 extern "C" int qt_frame_embed(const void* e0, const void* ecp, int dtype, int V0, int Vcp, int G, int H,
-                              const int* codes, long long codes_ld, const int* step, const float* trailing, int T,
-                              const float* pad, float* x, void* x16, int B, void* s) {
-  if (B <= 0 || H <= 0 || G < 1 || G > 32 || H % 8) return QT_ERR_SHAPE;
+                              const int* codes, long long codes_ld, const int* step, int step_stride,
+                              const float* trailing, int T, const float* pad, float* x, void* x16, int B, void* s) {
+  if (B <= 0 || H <= 0 || G < 1 || G > 32 || H % 8 || step_stride < 0) return QT_ERR_SHAPE;
   const dim3 grid(B, (H + 511) / 512);  // one wave per 512 dims
   if (dtype == QT_BF16)
     hipLaunchKernelGGL(frame_embed_k<bf16_t>, grid, dim3(64), 0, (hipStream_t)s, (const bf16_t*)e0,
-                       (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
+                       (const bf16_t*)ecp, V0, Vcp, G, H, codes, codes_ld, step, step_stride, trailing, T, pad, x, (bf16_t*)x16);
   else if (dtype == QT_F32)
     hipLaunchKernelGGL(frame_embed_k<float>, grid, dim3(64), 0, (hipStream_t)s, (const float*)e0,
-                       (const float*)ecp, V0, Vcp, G, H, codes, codes_ld, step, trailing, T, pad, x, (bf16_t*)x16);
+                       (const float*)ecp, V0, Vcp, G, H, codes, codes_ld, step, step_stride, trailing, T, pad, x, (bf16_t*)x16);
   else
     return QT_ERR_DTYPE;
   return ok();
@@ -199,6 +209,12 @@ extern "C" int qt_frame_embed(const void* e0, const void* ecp, int dtype, int V0
 extern "C" int qt_advance(int* c, int n, void* s) {
   if (n <= 0 || n > 1024) return QT_ERR_SHAPE;
   hipLaunchKernelGGL(advance_k, dim3(1), dim3(1024), 0, (hipStream_t)s, c, n);
+  return ok();
+}
+
+extern "C" int qt_advance_rows(int* c, int B, int nfields, int cap, void* s) {
+  if (B <= 0 || nfields <= 0) return QT_ERR_SHAPE;
+  hipLaunchKernelGGL(advance_rows_k, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)s, c, B, nfields, cap);
   return ok();
 }
 

@@ -120,8 +120,9 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   // compiler wait for each load in turn (one L2 round trip each).
   const bool pen = p.seen && p.rep_penalty != 1.0f;
   const unsigned char* sr = pen ? p.seen + (long long)r * V : (const unsigned char*)lg;
-  const int* ngp = p.n_generated ? p.n_generated : (const int*)lg;
-  const int* stpp = p.step ? p.step : (const int*)lg;
+  const int* ngp = p.n_generated ? p.n_generated + r * p.ctr_stride : (const int*)lg;
+  const int* stpp = p.step ? p.step + r * p.ctr_stride : (const int*)lg;
+  const int* prp = p.philox_row ? p.philox_row + r : (const int*)lg;
   const unsigned char* fnp = p.finished ? p.finished + r : (const unsigned char*)lg;
   const unsigned long long* sdp = p.seed_ptr ? p.seed_ptr : (const unsigned long long*)lg;
   float s[PER];
@@ -134,10 +135,12 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   const int str = __hip_atomic_load(stpp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int fnr = *fnp;
   const unsigned long long sdv = __hip_atomic_load(sdp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int prr = __hip_atomic_load(prp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int ngen = p.n_generated ? ngr : 1 << 30;
   const unsigned stp = p.step ? (unsigned)str : 0u;
   const int finv = p.finished ? fnr : 0;
   const unsigned long long seed = p.seed_ptr ? sdv : p.seed;
+  const unsigned prow = p.philox_row ? (unsigned)prr : (unsigned)(p.row_base + r);  // Philox stream id
   const bool eos_mask = p.eos_id >= 0 && (ngen < p.min_new_tokens || p.ignore_eos);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
           float best = -INFINITY;
           int bi = 0x7fffffff;
           auto draw = [&](float sc, int ti) {
-            const float u = philox_uniform4(seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)ti);
+            const float u = philox_uniform4(seed, stp, (unsigned)p.substep, prow, (unsigned)ti);
             const float g = okey_inv(okey(sc)) - __logf(-__logf(u));
             if (g > best || (g == best && ti < bi)) { best = g; bi = ti; }
           };
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
         const int mi = has ? ci_s[w][lane] : 0x7fffffff;
         float g = -INFINITY;
         if (has && mk > okey(-INFINITY)) {  // masked (-inf) scores are never drawn
-          const float u = philox_uniform4(seed, stp, (unsigned)p.substep, (unsigned)(p.row_base + r), (unsigned)mi);
+          const float u = philox_uniform4(seed, stp, (unsigned)p.substep, prow, (unsigned)mi);
           g = okey_inv(mk) - __logf(-__logf(u));
         }
         __syncthreads();
@@ -498,8 +501,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
       if (inc == 1234.5f) p.tok_out[r] = 0;
       return;
     }
-    const float uu = p.debug_u >= 0.f ? p.debug_u : philox_uniform(seed, stp, (unsigned)p.substep,
-                                                                   (unsigned)(p.row_base + r));
+    const float uu = p.debug_u >= 0.f ? p.debug_u : philox_uniform(seed, stp, (unsigned)p.substep, prow);
     const float u = uu * total;  // may round up to `total` itself
     if (tid == 0) shi[0] = -1;
     __syncthreads();
@@ -591,6 +593,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
 extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (!a || a->R <= 0 || a->V <= 0 || a->V > NT * 16 || !a->tok_out) return QT_ERR_SHAPE;
   if (a->do_sample && a->top_k > a->V) return QT_ERR_ARG;
+  if (a->ctr_stride < 0) return QT_ERR_SHAPE;
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
   if (a->emb_out16 && (!a->emb_table || a->emb_ld16 % 4)) return QT_ERR_SHAPE;
   if (a->emb2_table && (!a->emb_table || !a->emb2_out || a->emb2_dim % 4 || a->emb2_ld % 4)) return QT_ERR_SHAPE;

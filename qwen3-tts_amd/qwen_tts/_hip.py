@@ -80,7 +80,7 @@ class SampleArgs(ctypes.Structure):
                 ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll),
                 ("seed_ptr", c_void_p), ("debug_u", c_float), ("emb_out16", c_void_p), ("emb_ld16", c_ll),
                 ("emb2_table", c_void_p), ("emb2_dim", c_int), ("emb2_out", c_void_p), ("emb2_ld", c_ll),
-                ("algo", c_int)]
+                ("algo", c_int), ("ctr_stride", c_int), ("philox_row", c_void_p)]
 
 
 class MlpArgs(ctypes.Structure):
@@ -98,7 +98,7 @@ class CpMlpArgs(ctypes.Structure):
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj",
-           "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance",
+           "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
            "qt_scale_add", "qt_bcast_rows", "qt_cp_mlp", "qt_cp_mlp_tags_bytes", "qt_cp_mlp_supported"]
@@ -117,11 +117,12 @@ def load_library(path: str = LIB_PATH):
         "qt_gemm": [P, P], "qt_tile_weight": [P, c_int, c_int, c_int, P, P], "qt_qkv_post": [P, P],
         "qt_attention": [P, P], "qt_decode_attention": [P, P], "qt_sample": [P, P],
         "qt_rmsnorm": [P, P, c_float, P, c_int, c_int, P],
-        "qt_rmsnorm_rec": [P, P, c_float, P, c_int, c_int, P, c_ll, P, c_int, P],
+        "qt_rmsnorm_rec": [P, P, c_float, P, c_int, c_int, P, c_ll, P, c_int, c_int, P],
         "qt_small_prefill_attention": [P, c_int, P],
         "qt_gather_rows": [P, c_int, P, c_int, c_int, P, c_ll, P],
-        "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, P, c_int, P, P, P, c_int, P],
+        "qt_frame_embed": [P, P, c_int, c_int, c_int, c_int, c_int, P, c_ll, P, c_int, P, c_int, P, P, P, c_int, P],
         "qt_advance": [P, c_int, P],
+        "qt_advance_rows": [P, c_int, c_int, c_int, P],
         "qt_rvq_gather": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P],
         "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],

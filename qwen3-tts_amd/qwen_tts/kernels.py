@@ -281,8 +281,11 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
-           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None, algo=0):
-    """emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
+           codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None, algo=0,
+           ctr_stride=0, philox_row=None):
+    """step / n_generated: device int32 counters, one per row when ctr_stride = 1 (0: shared); philox_row: optional
+    device int32 [R] Philox stream ids (default row_base + r).
+    emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
     emb16 = (out bf16 rows, ld): its bf16 copy; emb2 = (table2 fp32 [V][D2], out2 fp32 rows, ld2): a second row.
     seed_ptr: device int64 [1] read at run time instead of `seed` (graph-captured samplers)."""
     a = _hip.SampleArgs()
@@ -296,6 +299,7 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     a.codes, a.codes_ld, a.codes_w, a.codes_col, a.codes_step_off = ptr(codes), codes_ld, codes_w, codes_col, codes_step_off
     a.row_base = row_base
     a.seed_ptr, a.debug_u, a.algo = ptr(seed_ptr), float(debug_u), int(algo)
+    a.ctr_stride, a.philox_row = int(ctr_stride), ptr(philox_row)
     if emb is not None:
         a.emb_table, a.emb_dim, a.emb_out, a.emb_ld = ptr(emb[0]), emb[0].shape[1], ptr(emb[1]), emb[2]
         if emb16 is not None:
@@ -305,13 +309,14 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 
-def rmsnorm(x, g, eps, out, M, N, rec=None, step=None, step_off=0):
-    """rec: also store the rows at rec[m, *step + step_off] (rec [M][F][N] fp32, step a device int32 counter)."""
+def rmsnorm(x, g, eps, out, M, N, rec=None, step=None, step_off=0, step_stride=0):
+    """rec: also store the rows at rec[m, step[m * step_stride] + step_off] (rec [M][F][N] fp32, step device int32
+    counters: one shared (stride 0) or one per row)."""
     if rec is None:
         check(_hip.lib().qt_rmsnorm(ptr(x), ptr(g), eps, ptr(out), M, N, stream()), "qt_rmsnorm")
     else:
         check(_hip.lib().qt_rmsnorm_rec(ptr(x), ptr(g), eps, ptr(out), M, N, ptr(rec), rec.stride(0), ptr(step),
-                                        step_off, stream()), "qt_rmsnorm_rec")
+                                        step_off, step_stride, stream()), "qt_rmsnorm_rec")
 
 
 def gather_rows(table, idx, M, H, out, ldo):
@@ -319,15 +324,21 @@ def gather_rows(table, idx, M, H, out, ldo):
           "qt_gather_rows")
 
 
-def frame_embed(e0, ecp, G, H, codes, codes_ld, step, trailing, T, pad, x, B, x16=None):
+def frame_embed(e0, ecp, G, H, codes, codes_ld, step, trailing, T, pad, x, B, x16=None, step_stride=0):
     check(_hip.lib().qt_frame_embed(ptr(e0), ptr(ecp), _hip.dtype_code(e0.dtype), e0.shape[0], ecp.shape[1], G, H,
-                                    ptr(codes), codes_ld, ptr(step), ptr(trailing), T, ptr(pad), ptr(x), ptr(x16), B,
+                                    ptr(codes), codes_ld, ptr(step), step_stride, ptr(trailing), T, ptr(pad), ptr(x),
+                                    ptr(x16), B,
                                     stream()),
           "qt_frame_embed")
 
 
 def advance(counters, n):
     check(_hip.lib().qt_advance(ptr(counters), n, stream()), "qt_advance")
+
+
+def advance_rows(counters, B, nfields, cap):
+    """Per-row counters [nfields][B] (field 0 = frame index): rows below cap advance every field by one."""
+    check(_hip.lib().qt_advance_rows(ptr(counters), B, nfields, cap, stream()), "qt_advance_rows")
 
 
 def rvq_gather(tables, Q, n_first, cb, dim, codes, B, T, o1, o2):

@@ -216,13 +216,26 @@ class TTSModel:
                  speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                  temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                  subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
-                 use_graph=True, **kwargs):
+                 use_graph=True, max_batch=None, **kwargs):
         """Same contract as Qwen3TTSForConditionalGeneration.generate (M:2022-2292):
-        returns (list of [F_i,16] int64 codes, list of [F_i,H] last hidden states)."""
+        returns (list of [F_i,16] int64 codes, list of [F_i,H] last hidden states).
+
+        max_batch (not in the reference): with more requests than max_batch, decode them by continuous batching
+        through max_batch batch rows (TalkerEngine.serve: a row is refilled with the next request as soon as its
+        request ends).  Per request the result is that of the one-shot batched call (same Philox stream per request
+        index; per-row arithmetic does not depend on the batch's other rows)."""
         emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
                                                    voice_clone_prompt, ref_ids)
         gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
                        subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
+        B, P = emb.shape[0], emb.shape[1]
+        if max_batch is not None and B > int(max_batch):
+            n_real = mask.sum(-1).tolist()
+            reqs = [(emb[i, P - int(n_real[i]):], trail[i]) for i in range(B)]
+            codes, hid = [None] * B, [None] * B
+            for i, c, h in self.engine.serve(reqs, pad, gp, slots=int(max_batch), use_graph=use_graph):
+                codes[i], hid[i] = c, h
+            return codes, hid
         return self.engine.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=use_graph)
 
     # -------------------------------------------------------------------------------- streaming

@@ -248,12 +248,15 @@ class Session:
         self.cp_L = self.G + 1
         self.cp_kv = ([torch.zeros(B, c.Hkv, self.cp_L, c.D, dtype=kvd, device=dev) for _ in range(c.n_layers)],
                       [torch.zeros(B, c.Hkv, self.cp_L, c.D, dtype=kvd, device=dev) for _ in range(c.n_layers)])
-        # counters: [step, n_generated, rope_pos[B], kv_pos[B], kv_len[B]] advanced together each frame
-        self.ctr = i32(2 + 3 * B)
-        self.step, self.n_gen = self.ctr[0:1], self.ctr[1:2]
-        self.meta = {"rope_pos": self.ctr[2:2 + B], "kv_pos": self.ctr[2 + B:2 + 2 * B],
-                     "row_len": self.ctr[2 + 2 * B:2 + 3 * B], "row_start": i32(B),
+        # per-row counters, field-major [5][B]: frame index (step), n_generated, rope_pos, kv_pos, kv_len -- every row
+        # its own request clock, so a batch slot can be refilled with a new request mid-decode (serve()); a row
+        # advances until its frame index reaches max_frames (qt_advance_rows)
+        self.ctr = i32(5 * B)
+        self.step, self.n_gen = self.ctr[0:B], self.ctr[B:2 * B]
+        self.meta = {"rope_pos": self.ctr[2 * B:3 * B], "kv_pos": self.ctr[3 * B:4 * B],
+                     "row_len": self.ctr[4 * B:5 * B], "row_start": i32(B),
                      "row_batch": torch.arange(B, dtype=torch.int32, device=dev)}
+        self.prow = torch.arange(B, dtype=torch.int32, device=dev)  # Philox stream id of each row's request
         f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.x = f32(B, t.H)
         # bf16 shadows of the decode residual streams (bf16 mode): A operands of the RMS-normalised GEMVs
@@ -266,7 +269,7 @@ class Session:
         self.cp_x = f32(2 * B, c.H)
         self.sc_t = _scratch(B, t, dev)
         self.codes = i32(B, max_frames + 2, self.G)
-        self.hiddens = f32(B, max_frames + 1, t.H)
+        self.hiddens = f32(B, max_frames + 2, t.H)  # + the frame a capped row re-runs (serve())
         self.tok0 = i32(B)
         self.cp_tok = i32(B)
         self.seen = torch.zeros(B, eng.V, dtype=torch.uint8, device=dev)
@@ -278,6 +281,7 @@ class Session:
         self.row_base = 0
         self.graph = None
         self.prefill = {}  # prompt length P -> static prefill buffers (+ captured graph once P repeats)
+        self.slot_prefill = {}  # prompt length P -> static single-request prefill buffers (serve() refills)
         self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
         nl = max(1, min(eng.cp_lanes, B))
         cuts = [B * i // nl for i in range(nl + 1)]
@@ -428,17 +432,21 @@ class TalkerEngine:
     def _eos(self, gp):
         return gp.eos_token_id if gp.eos_token_id is not None else self.tc["codec_eos_token_id"]
 
-    def _sample_talker(self, s: Session, logits, codes_step_off, substep):
+    def _sample_talker(self, s: Session, logits, codes_step_off, substep, b0=0, b1=None):
+        """Talker token choice for rows [b0, b1) of the session (default all)."""
         gp = s.gp
         eos = self._eos(gp)
-        K.sample(logits, s.B, self.V, self.V, s.tok0, seen=s.seen, rep_penalty=gp.repetition_penalty,
-                 n_generated=s.n_gen, min_new_tokens=2, eos_id=eos,
+        b1 = s.B if b1 is None else b1
+        Hc = self.cp.H
+        K.sample(logits[b0:b1], b1 - b0, self.V, self.V, s.tok0[b0:b1], seen=s.seen[b0:b1],
+                 rep_penalty=gp.repetition_penalty, n_generated=s.n_gen[b0:b1], min_new_tokens=2, eos_id=eos,
                  suppress=(self.V - 1024, self.V, self.tc["codec_eos_token_id"]), ignore_eos=gp.ignore_eos,
-                 finished=s.finished, do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
-                 temperature=gp.temperature, seed_ptr=s.seed, step=s.step, substep=substep, codes=s.codes,
-                 codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0, codes_step_off=codes_step_off,
-                 row_base=s.row_base, emb=(self.cp_in_tab0, s.cp_x.view(-1)[self.cp.H:], 2 * self.cp.H),
-                 emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[self.cp.H:], 2 * self.cp.H))
+                 finished=s.finished[b0:b1], do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
+                 temperature=gp.temperature, seed_ptr=s.seed, step=s.step[b0:b1], substep=substep,
+                 codes=s.codes[b0:b1], codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0,
+                 codes_step_off=codes_step_off, ctr_stride=1, philox_row=s.prow[b0:b1],
+                 emb=(self.cp_in_tab0, s.cp_x.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc),
+                 emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc))
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
@@ -462,13 +470,13 @@ class TalkerEngine:
                 main.wait_stream(self._cp_streams[i - 1])
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
-                      s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16)
+                      s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
         t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
         # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])
-        K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1)
+        K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1, step_stride=1)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
         self._sample_talker(s, s.logits, 1, 0)
-        K.advance(s.ctr, 2 + 3 * B)
+        K.advance_rows(s.ctr, B, 5, s.max_frames)
 
     def _cp_lane(self, s: Session, ln: CPLane):
         """Code predictor for rows [b0, b1): 2-token prefill + 14 decode steps (M:1671-1680)."""
@@ -503,8 +511,9 @@ class TalkerEngine:
             K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
-                 seed_ptr=s.seed, step=s.step, substep=1 + g, codes=ln.codes, codes_ld=s.codes.shape[1] * self.G,
-                 codes_w=self.G, codes_col=1 + g, codes_step_off=0, row_base=s.row_base + ln.b0,
+                 seed_ptr=s.seed, step=s.step[ln.b0:ln.b1], substep=1 + g, codes=ln.codes,
+                 codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=1 + g, codes_step_off=0, ctr_stride=1,
+                 philox_row=s.prow[ln.b0:ln.b1],
                  emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None,
                  emb16=(ln.x16, c.H) if ln.x16 is not None and g < self.G - 2 else None,
                  emb2=(self.cp_qkv_tabs[g], ln.sc["qkv"], c.qkv_w) if self.cp_qkv_tabs is not None and g < self.G - 2
@@ -629,6 +638,154 @@ class TalkerEngine:
                 out_h.append(hid[b, :L])
         return out_c, out_h
 
+    # ---------------------------------------------------------------- continuous batching
+    def serve(self, requests, tts_pad, gp: GenParams, slots: int = 8, use_graph: bool = True, poll: int = 4):
+        """Continuous batching: decode `requests` through `slots` batch rows of one session, refilling a row with
+        the next queued request as soon as its request ends (EOS, or max_new_tokens - 1 frames) instead of padding
+        it with EOS until the whole batch ends as the reference's batched generate() does (M:2272-2292).
+
+        requests: list of (embeds fp32 [P_i, H], trailing fp32 [T_i, H][, frames_i]) -- one unpadded prompt each (a
+        row of build_prompts() with its left padding removed); the optional frames_i caps that request below
+        max_new_tokens - 1 frames (it is retired at the first poll past it, so its row may run up to `poll` frames
+        longer).  Yields (i, codes [F_i, 16] int64 cpu, hidden [F_i, H] cpu)
+        as requests finish (completion order).  Request i draws Philox stream i of the call's seed, i.e. the
+        stream row i of a one-shot batched generate() of the same list draws, whichever slot decodes it.
+
+        The frame graph is the session's ordinary captured frame (per-row step / position counters); a refill is
+        a single-request prefill into the slot's K/V rows between two graph replays.  The host learns which rows
+        ended from pinned copies of the device flags every `poll` frames (no host sync on the decode stream)."""
+        n = len(requests)
+        if n == 0:
+            return
+        B = max(1, min(slots, n))
+        ahead = 1
+        max_frames = max(gp.max_new_tokens - 1, 1)
+        P = max(int(r[0].shape[0]) for r in requests)
+        cap_i = [min(max_frames, int(r[2])) if len(r) > 2 and r[2] is not None else max_frames for r in requests]
+        seed = gp.resolve_seed()
+        eos = self.tc["codec_eos_token_id"]
+        s = self.session(B, P, max_frames, gp)
+        H, dev = self.talker.H, self.dev
+        try:
+            with K.use_workspace(s.ws):
+                # the first B requests start together: one left-padded batched prefill (as generate() does)
+                Pb = max(int(r[0].shape[0]) for r in requests[:B])
+                Tb = max(int(r[1].shape[0]) for r in requests[:B])
+                emb = torch.zeros(B, Pb, H, dtype=torch.float32, device=dev)
+                mask = torch.zeros(B, Pb, dtype=torch.long, device=dev)
+                trail = tts_pad.reshape(1, 1, H).float().to(dev).repeat(B, Tb, 1)
+                for b in range(B):
+                    e, tr = requests[b][0], requests[b][1]
+                    emb[b, Pb - e.shape[0]:] = e
+                    mask[b, Pb - e.shape[0]:] = 1
+                    trail[b, :tr.shape[0]] = tr
+                self._prefill(s, emb, mask, trail, tts_pad, seed)
+                s.hiddens[:, 0].copy_(s.past_hidden)
+                queue = list(range(B, n))
+                slot_req = list(range(B))
+                epoch = [0] * B
+                start = [0] * B  # host frame count when the slot's request started
+                if use_graph and s.graph is None:
+                    s.graph = self._capture(s)
+                polls, harvests = [], []
+                frame = 0
+                while any(r >= 0 for r in slot_req) or harvests:
+                    if any(r >= 0 for r in slot_req):
+                        if use_graph:
+                            s.graph.replay()
+                        else:
+                            self._frame(s)
+                        frame += 1
+                        if frame % poll == 0 and not gp.ignore_eos:  # (with ignore_eos only frame counts end rows)
+                            st = torch.empty(2 * B, dtype=torch.int32, pin_memory=True)
+                            st[:B].copy_(s.step, non_blocking=True)
+                            st[B:].copy_(s.finished, non_blocking=True)
+                            ev = torch.cuda.Event()
+                            ev.record()
+                            polls.append((st, list(epoch), ev))
+                    else:  # only harvests left in flight
+                        harvests[0][-1].synchronize()
+                    # rows that ended (as of a completed poll, same request still in the slot): copy their codes out
+                    # and refill the slot, both in stream order behind the frames already queued.  The host may run
+                    # at most `ahead` polls in front of the GPU (else it would queue many frames past a row's end
+                    # before seeing it, and that row's slot would idle for all of them)
+                    ended = [b for b in range(B) if slot_req[b] >= 0 and frame - start[b] >= cap_i[slot_req[b]]]
+                    while polls and (len(polls) > ahead or polls[0][2].query()):
+                        polls[0][2].synchronize()
+                        st, ep, _ = polls.pop(0)
+                        ended += [b for b in range(B) if slot_req[b] >= 0 and ep[b] == epoch[b] and int(st[B + b])]
+                    # a row whose request reached its frame count is known on the host without a poll (its frame
+                    # index = frames replayed since it started); EOS is learned from the polls
+                    for b in sorted(set(ended)):
+                        hc = torch.empty(s.codes.shape[1], self.G, dtype=torch.int32, pin_memory=True)
+                        hh = torch.empty(s.hiddens.shape[1], H, dtype=torch.float32, pin_memory=True)
+                        hs = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                        hc.copy_(s.codes[b], non_blocking=True)
+                        hh.copy_(s.hiddens[b], non_blocking=True)
+                        hs.copy_(s.step[b:b + 1], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        harvests.append((slot_req[b], hc, hh, hs, ev))
+                        epoch[b] += 1
+                        start[b] = frame
+                        slot_req[b] = queue.pop(0) if queue else -1
+                        if slot_req[b] >= 0:
+                            self._prefill_slot(s, b, requests[slot_req[b]], slot_req[b])
+                        else:
+                            s.finished[b:b + 1].fill_(1)  # idle slot: emits EOS until the session ends
+                    while harvests and harvests[0][-1].query():
+                        i, hc, hh, hs, _ = harvests.pop(0)
+                        # frames [0, F) are final: F = the first EOS in cb0 (within the row's frame range), else the
+                        # row's frame count (max_new_tokens - 1)
+                        F = min(int(hs[0]), cap_i[i])
+                        hit = (hc[:F + 1, 0] == eos).nonzero()
+                        F = int(hit[0]) if hit.numel() else F
+                        yield i, hc[:F].long(), hh[:F].clone()
+                self.serve_stats = {"frames": frame, "slots": B, "requests": n}
+        finally:
+            self.release([s])
+
+    def _prefill_slot(self, s: Session, b: int, req, i: int):
+        """Start request i in batch row b: per-row state reset, single-request talker prefill into row b's K/V
+        (positions 0..P-1, no left padding), first token (M:1746-1800, 2044)."""
+        emb, trail = req[0], req[1]
+        P, H = int(emb.shape[0]), self.talker.H
+        t, dev = self.talker, self.dev
+        if P + s.max_frames + 2 > s.Lmax:
+            raise ValueError(f"prompt of {P} tokens exceeds the session's K/V capacity ({s.Lmax})")
+        for z in (s.seen, s.finished, s.codes):
+            z[b].zero_()
+        s.prow[b:b + 1].fill_(i)
+        s.meta["row_start"][b:b + 1].zero_()
+        c = s.ctr.view(5, s.B)
+        c[0, b:b + 1].zero_()
+        c[1, b:b + 1].fill_(1)
+        c[2:4, b:b + 1].fill_(P)
+        c[4, b:b + 1].fill_(P + 1)
+        tr = s.trailing[b]
+        tr.copy_(s.pad_embed.view(1, H).expand_as(tr))
+        nt = min(int(trail.shape[0]), tr.shape[0])
+        tr[:nt] = trail[:nt].to(dev).float()
+        pre = s.slot_prefill.get(P)
+        if pre is None:
+            i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
+            ar = torch.arange(P, device=dev, dtype=torch.int32)
+            pre = {"x": torch.empty(P, H, dtype=torch.float32, device=dev), "sc": _scratch(P, t, dev),
+                   "meta": {"rope_pos": ar, "kv_pos": ar.clone(), "row_len": ar + 1, "row_start": i32(P),
+                            "row_batch": i32(P)},
+                   "x16": (torch.empty(P, H, dtype=torch.bfloat16, device=dev)
+                           if X16 and self.wdt == torch.bfloat16 and P <= 96 else None)}
+            s.slot_prefill[P] = pre
+        pre["meta"]["row_batch"].fill_(b)
+        pre["x"].copy_(emb.reshape(P, H))
+        if pre["x16"] is not None:
+            pre["x16"].copy_(pre["x"])
+        t.forward(pre["x"], P, pre["meta"], s.kv, pre["sc"], s.Lmax, P, x16=pre["x16"])
+        K.rmsnorm(pre["x"][P - 1:], t.norm, t.eps, s.past_hidden[b:b + 1], 1, H)
+        s.hiddens[b, 0].copy_(s.past_hidden[b])
+        K.gemm(s.past_hidden[b:b + 1], self.codec_head, s.logits[b:b + 1], 1, H, self.V)
+        self._sample_talker(s, s.logits, 0, 99, b, b + 1)
+
     def _prefill(self, s: Session, embeds, mask, trailing, tts_pad, seed: int):
         """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s."""
         B, P, H = embeds.shape
@@ -638,6 +795,7 @@ class TalkerEngine:
         for z in (s.seen, s.finished, s.codes, s.ctr):
             z.zero_()
         s.seed.fill_(seed)
+        torch.arange(s.row_base, s.row_base + B, dtype=torch.int32, device=dev, out=s.prow)
         # stale K/V beyond each row's valid range is never read (row_start/row_len bound every read)
         Ttr = trailing.shape[1]
         s.pad_embed.copy_(tts_pad.reshape(-1).float())
@@ -680,7 +838,7 @@ class TalkerEngine:
             if PREFILL_GRAPH and pre["uses"] >= 2:
                 pre["graph"] = self._capture_prefill(s, pre, B, P)
         # decode counters: step 0, one token generated, pos = P + delta, kv_pos = P, len = P + 1
-        s.ctr[1:2].fill_(1)  # a device fill: item assignment uploads a host scalar and waits for the prefill
+        s.n_gen.fill_(1)  # a device fill: item assignment uploads a host scalar and waits for the prefill
         s.meta["rope_pos"].copy_((P + rope_delta).to(torch.int32))
         s.meta["kv_pos"].fill_(P)
         s.meta["row_len"].fill_(P + 1)

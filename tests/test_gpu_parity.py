@@ -1170,3 +1170,47 @@ def test_cp_mlp_pipeline_tracks_launch_path(monkeypatch):
     for a, b in zip(out[False], out[True]):
         assert a.shape == b.shape
         assert torch.equal(a[0], b[0])  # later codes may follow a flipped near-tie into a different continuation
+
+
+def _serve_case():
+    return dict(texts=[7, 3, 10, 5, 12, 4], languages=["auto", "english", "japanese", "chinese", "english", "auto"],
+                speakers=["vivian", None, "dylan", "eric", "ryan", ""], non_streaming_mode=False, max_new_tokens=40)
+
+
+@pytest.mark.parametrize("dtype,sample", [("fp32", False), ("fp32", True), ("bf16", True)])
+def test_continuous_batching_matches_one_shot(tiny_models, dtype, sample):
+    """generate(max_batch=k) decodes 6 requests through k batch rows, refilling a row as soon as its request ends
+    (TalkerEngine.serve); every request's codes and hidden states equal the one-shot batched call's
+    (EOS-ragged lengths, per-request Philox streams when sampling)."""
+    from cases import make_inputs
+    from qwen_tts.model import TTSModel
+    z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    W = dict(W)
+    head = W["talker.codec_head.weight"].clone()
+    head[cfg["talker_config"]["codec_eos_token_id"]] = head[int(z["eos_b2/donor"])]
+    W["talker.codec_head.weight"] = head
+    model = TTSModel(cfg, W, dtype=dtype)
+    case = _serve_case()
+    ids, _, _, _ = make_inputs(case, 11, cfg["talker_config"]["hidden_size"])
+    kw = dict(input_ids=ids, languages=case["languages"], speakers=case["speakers"], non_streaming_mode=False,
+              max_new_tokens=case["max_new_tokens"], do_sample=sample, subtalker_dosample=sample, seed=7)
+    ref, ref_h = model.generate(**kw)
+    assert len({c.shape[0] for c in ref}) > 1  # EOS-ragged
+    for mb in (1, 2, 4):
+        codes, hid = model.generate(**kw, max_batch=mb)
+        assert len(codes) == len(ref)
+        for i, (a, b) in enumerate(zip(codes, ref)):
+            np.testing.assert_array_equal(a.numpy(), b.numpy(), err_msg=f"max_batch={mb} request {i}")
+            np.testing.assert_allclose(hid[i].numpy(), ref_h[i].numpy(), atol=1e-5, rtol=1e-5)
+
+
+def test_advance_rows_caps_each_row():
+    from qwen_tts import kernels as K
+    dev = _dev()
+    B = 5
+    c = torch.arange(5 * B, dtype=torch.int32, device=dev)  # field 0 = [0, 1, 2, 3, 4]
+    ref = c.clone().view(5, B)
+    K.advance_rows(c, B, 5, 3)
+    ref[:, :3] += 1  # rows with frame index < 3 advance every field; rows 3, 4 stay
+    torch.testing.assert_close(c.view(5, B), ref)
