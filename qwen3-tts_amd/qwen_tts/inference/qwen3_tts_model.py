@@ -229,6 +229,45 @@ class Qwen3TTSModel:
     @torch.no_grad()
     def generate_voice_clone(self, text, language=None, ref_audio=None, ref_text=None, x_vector_only_mode=False,
                              voice_clone_prompt=None, non_streaming_mode=False, **kwargs):
+        input_ids, ref_ids, vcp, languages = self._voice_clone_inputs(text, language, ref_audio, ref_text,
+                                                                      x_vector_only_mode, voice_clone_prompt)
+        codes, _ = self.model.generate(input_ids=input_ids, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=languages,
+                                       non_streaming_mode=non_streaming_mode, **self._merge_generate_kwargs(**kwargs))
+        refs = vcp.get("ref_code", None)
+        dec = [torch.cat([refs[i].cpu().long(), c], 0) if refs is not None and refs[i] is not None else c
+               for i, c in enumerate(codes)]
+        wavs, fs = self._decode(dec)
+        out = []
+        for i, w in enumerate(wavs):
+            if refs is not None and refs[i] is not None:
+                cut = int(int(refs[i].shape[0]) / max(int(dec[i].shape[0]), 1) * w.shape[0])
+                out.append(w[cut:])
+            else:
+                out.append(w)
+        return out, fs
+
+    @torch.no_grad()
+    def stream_voice_clone(self, text, language=None, ref_audio=None, ref_text=None, x_vector_only_mode=False,
+                           voice_clone_prompt=None, non_streaming_mode=False, first_chunk_frames=2, chunk_frames=48,
+                           **kwargs):
+        """New surface (no reference counterpart, SURVEY.md §8f-1 + 8f-2): streaming voice clone.  Same inputs as
+        generate_voice_clone (reference audio is encoded / x-vectored at submit); yields (utterance index, pcm chunk
+        np.float32, sample rate, is_last).  Per utterance the chunks concatenate to generate_voice_clone()'s PCM: in
+        ICL mode the reference codes are decoded in front of the generated ones and the output starts at their
+        boundary -- the wrapper's proportional cut keeps floor(555 R / T) more samples of the reference's tail, a
+        length-dependent point a stream cannot know in advance (TTSModel._stream_stateful)."""
+        input_ids, ref_ids, vcp, languages = self._voice_clone_inputs(text, language, ref_audio, ref_text,
+                                                                      x_vector_only_mode, voice_clone_prompt)
+        sr = self.model.speech_tokenizer.get_output_sample_rate()
+        for i, pcm, last in self.model.stream(input_ids=input_ids, ref_ids=ref_ids, voice_clone_prompt=vcp,
+                                              languages=languages, non_streaming_mode=non_streaming_mode,
+                                              first_chunk_frames=first_chunk_frames, chunk_frames=chunk_frames,
+                                              **self._merge_generate_kwargs(**kwargs)):
+            yield i, pcm.to(torch.float32).cpu().numpy(), sr, last
+
+    def _voice_clone_inputs(self, text, language, ref_audio, ref_text, x_vector_only_mode, voice_clone_prompt):
+        """W:460-633 input handling of generate_voice_clone: -> (input_ids, ref_ids, voice_clone_prompt dict,
+        languages)."""
         if self.model.tts_model_type != "base":
             raise ValueError(f"model with tts_model_type: {self.model.tts_model_type} does not support "
                              "generate_voice_clone, Please check Model Card or Readme for more details.")
@@ -258,20 +297,7 @@ class Qwen3TTSModel:
         ref_ids = None
         if ref_texts is not None:
             ref_ids = [None if not rt else self._tokenize_texts([self._build_ref_text(rt)])[0] for rt in ref_texts]
-        codes, _ = self.model.generate(input_ids=input_ids, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=languages,
-                                       non_streaming_mode=non_streaming_mode, **self._merge_generate_kwargs(**kwargs))
-        refs = vcp.get("ref_code", None)
-        dec = [torch.cat([refs[i].cpu().long(), c], 0) if refs is not None and refs[i] is not None else c
-               for i, c in enumerate(codes)]
-        wavs, fs = self._decode(dec)
-        out = []
-        for i, w in enumerate(wavs):
-            if refs is not None and refs[i] is not None:
-                cut = int(int(refs[i].shape[0]) / max(int(dec[i].shape[0]), 1) * w.shape[0])
-                out.append(w[cut:])
-            else:
-                out.append(w)
-        return out, fs
+        return input_ids, ref_ids, vcp, languages
 
     # ---------------------------------------------------------------- voice design (W:637-728)
     @torch.no_grad()

@@ -276,10 +276,15 @@ class TTSModel:
         cum = [0] * B                     # samples emitted per row
         # chunk sizes double from first_chunk_frames up to chunk_frames: each chunk's audio (80 ms per frame) covers
         # the generation of the next one (~3 ms per frame), so playback started at the first packet never starves
+        refs = voice_clone_prompt.get("ref_code") if voice_clone_prompt is not None else None
+        prefix = None if refs is None or all(r is None for r in refs) else list(refs)
         if left_context is None:
             yield from self._stream_stateful(dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames,
-                                             use_graph)
+                                             use_graph, prefix)
             return
+        if prefix is not None:
+            raise NotImplementedError("stream(left_context=...) with voice-clone reference codes (ICL): use the "
+                                      "default stateful stream")
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames + 1, grow=True)
         for sessions, frames, final in it:
@@ -331,19 +336,58 @@ class TTSModel:
             if all(done):
                 break
 
-    def _stream_stateful(self, dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames, use_graph):
+    @staticmethod
+    def _stream_window(codes, pre, R, end, lo, hi):
+        """Decode positions [lo, hi) of every row's sequence prefix_b + generated_b + zeros, int32 [B, hi-lo, 16]
+        (generated frame f of row b sits at position R_b + f; rows past their end are the batch decode's zero
+        padding)."""
+        B = codes.shape[0]
+        if not any(R):
+            cc = codes[:, lo:hi].clone()
+            for b in range(B):
+                if end[b] is not None and end[b] < hi:
+                    cc[b, max(end[b] - lo, 0):] = 0
+            return cc
+        cc = torch.zeros(B, hi - lo, codes.shape[2], dtype=codes.dtype, device=codes.device)
+        for b in range(B):
+            if R[b] > lo:  # prefix part
+                cc[b, :min(R[b], hi) - lo] = pre[b][lo:min(R[b], hi)]
+            g0, g1 = max(lo, R[b]) - R[b], hi - R[b]  # generated frames [g0, g1)
+            if end[b] is not None:
+                g1 = min(g1, end[b])
+            if g1 > g0:
+                cc[b, g0 + R[b] - lo:g1 + R[b] - lo] = codes[b, g0:g1]
+        return cc
+
+    def _stream_stateful(self, dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames, use_graph,
+                         prefix=None):
         """stream() on the incremental codec: every final frame is fed once to the decoder of its reference chunk
         and every sample computable from the frames fed so far is emitted -- 1920 n - 555 samples of a chunk after
         its n frames, i.e. no lookahead frame is waited for (the 555 samples that need it follow with the next
-        chunk; at a reference chunk's end they are dropped, as the reference's chunked decode drops them)."""
+        chunk; at a reference chunk's end they are dropped, as the reference's chunked decode drops them).
+
+        prefix[b] (voice clone, ICL mode): the reference codes int [R_b, 16] that generate_voice_clone decodes in
+        front of row b's generated codes (W:263-274, `cat(ref_code, codes)` then a proportional cut).  Row b's decode
+        sequence is then ref_b + generated + zero padding; the ref frames are known at submit and fed with the first
+        chunk, and row b's output starts at sample 1920 R_b of its sequence, the reference/generated boundary.  The
+        wrapper's proportional cut int(R_b / T_b * len_b) lands floor(555 R_b / T_b) samples earlier (len_b lacks
+        the last frame's 555 lookahead samples), at a point that depends on the final length T_b, which a stream
+        does not know when it starts: the streamed PCM is generate_voice_clone's PCM without those leading samples
+        (< 555, e.g. 72 for 38 reference frames + 256 generated)."""
         up = dec.total_upsample
         RC, RX = self.REF_CHUNK, self.REF_CTX
-        end = [None] * B                  # frame count of each row once its EOS is seen
-        cap = [None] * B                  # one-shot sample count (1920 x #nonzero cb0) once the row has ended
+        dev = self.device
+        pre = [None] * B if prefix is None else [None if x is None else torch.as_tensor(x).to(dev, torch.int32)
+                                                  for x in prefix]
+        R = [0 if x is None else int(x.shape[0]) for x in pre]
+        pre_nz = [0 if x is None else int((x[:, 0] != 0).sum()) for x in pre]
+        end = [None] * B                  # generated frame count of each row once its EOS is seen
+        cap = [None] * B                  # one-shot sample count (1920 x #nonzero cb0 of its sequence) once ended
         done = [False] * B
-        cum = [0] * B                     # samples emitted per row
+        skip = [up * r for r in R]        # samples of row b's sequence before its output starts
+        gpos = 0                          # samples of the (shared) decode timeline produced so far
         scanned = 0                       # cb0 columns already searched for EOS
-        k, cs, fed, emit_s, ctx_s = 0, None, 0, 0, 0   # reference chunk, its decoder, frames fed, samples emitted
+        k, cs, fed, emit_s, ctx_s = 0, None, 0, 0, 0   # reference chunk, its decoder, positions fed, samples emitted
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames, grow=True)
         try:
@@ -359,10 +403,11 @@ class TTSModel:
                     if final and end[b] is None:
                         end[b] = frames
                     if end[b] is not None and cap[b] is None:
-                        cap[b] = up * int((c0[b, :end[b]] != 0).sum())
+                        cap[b] = up * (pre_nz[b] + int((c0[b, :end[b]] != 0).sum()))
                 scanned = frames
-                t_end = max(end) if all(x is not None for x in end) else None
-                avail = t_end if t_end is not None else frames
+                # decode positions (prefix + generated) available for every row; the sequence length once all ended
+                t_end = max(R[b] + end[b] for b in range(B)) if all(x is not None for x in end) else None
+                avail = t_end if t_end is not None else min(R[b] + frames for b in range(B) if end[b] is None)
                 while True:
                     cend = (k + 1) * RC
                     if cs is None:  # reference chunk k: a fresh decoder, primed from its 25 context frames
@@ -370,10 +415,7 @@ class TTSModel:
                         cs, fed, emit_s, ctx_s = dec.stream(B, RX + RC), base, 0, (k * RC - base) * up
                     hi = min(avail, cend)
                     if hi > fed:
-                        cc = codes[:, fed:hi].clone()
-                        for b in range(B):  # finished rows continue as the one-shot batch decode's zero padding
-                            if end[b] is not None and end[b] < hi:
-                                cc[b, max(end[b] - fed, 0):] = 0
+                        cc = self._stream_window(codes, pre, R, end, fed, hi)
                         cs.feed(cc)
                         fed = hi
                     n = max(cs.ns - ctx_s - emit_s, 0)
@@ -381,13 +423,17 @@ class TTSModel:
                     for b in range(B):
                         if done[b] or n == 0:
                             continue
-                        take = n if cap[b] is None else max(0, min(n, cap[b] - cum[b]))
-                        chunk = cs.pcm[b, ctx_s + emit_s:ctx_s + emit_s + take]
-                        cum[b] += take
-                        last = cap[b] is not None and (cum[b] >= cap[b] or ended)
+                        lo_s = max(gpos, skip[b])
+                        hi_s = gpos + n if cap[b] is None else min(gpos + n, cap[b])
+                        last = cap[b] is not None and (gpos + n >= cap[b] or ended)
+                        if hi_s <= lo_s and not last:
+                            continue
+                        o = ctx_s + emit_s + (lo_s - gpos)
+                        chunk = cs.pcm[b, o:o + max(hi_s - lo_s, 0)]
                         done[b] = last
                         yield b, chunk, last
                     emit_s += n
+                    gpos += n
                     if fed == cend and not ended:  # chunk k complete (its 555-sample tail is dropped): next chunk
                         cs.close()
                         cs, k = None, k + 1

@@ -1214,3 +1214,44 @@ def test_advance_rows_caps_each_row():
     K.advance_rows(c, B, 5, 3)
     ref[:, :3] += 1  # rows with frame index < 3 advance every field; rows 3, 4 stay
     torch.testing.assert_close(c.view(5, B), ref)
+
+
+@pytest.mark.parametrize("frames", [30, 331])
+def test_stream_voice_clone_matches_wrapper(tiny_models, frames):
+    """stream() with a voice-clone prompt (row 0 ICL with 7 reference code frames, row 1 x-vector only): per row the
+    chunks concatenate to generate_voice_clone's decode of cat(ref_code, codes) (W:263-274) from the
+    reference/generated boundary on, including a > 300-frame sequence whose reference chunk restart falls inside the
+    generated part."""
+    from cases import gen_kwargs, make_inputs, talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    _dev()
+    cfg, W, model = tiny_models["tiny-customvoice"]
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    tok = Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer", dtype="fp32", weights=CW)
+    model.load_speech_tokenizer(tok)
+    key = "icl_b2"
+    case = dict(talker_cases()[key], max_new_tokens=frames)
+    ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
+    kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=case["languages"],
+              speakers=case["speakers"], non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+    codes, _ = model.generate(**kw)
+    refs = vcp["ref_code"]
+    dec = [torch.cat([refs[i].long(), c], 0) if refs[i] is not None else c for i, c in enumerate(codes)]
+    wavs, _ = tok.decode([{"audio_codes": c} for c in dec])
+    chunks = {}
+    for b, pcm, last in model.stream(first_chunk_frames=2, chunk_frames=8, **kw):
+        chunks.setdefault(b, []).append(pcm.cpu().numpy())
+    up = model.speech_tokenizer.model.total_upsample
+    for b, w in enumerate(wavs):
+        R = 0 if refs[b] is None else int(refs[b].shape[0])
+        cut = int(R / dec[b].shape[0] * w.shape[0]) if R else 0
+        # the wrapper's proportional cut lands floor(555 R / T) samples before the reference/generated boundary (its
+        # decoded length lacks the last frame's 555 lookahead samples) -- a point that moves with the final length
+        # T; the stream starts at the boundary itself, so it equals the wrapper's PCM without those samples
+        assert 0 <= up * R - cut <= 555, (cut, up * R)
+        want = w[up * R:]
+        got = np.concatenate(chunks[b])
+        assert got.shape == want.shape, (b, got.shape, want.shape)
+        np.testing.assert_allclose(got, want, atol=2e-4, rtol=0)
