@@ -248,7 +248,7 @@ class Qwen3TTSModel:
 
     @torch.no_grad()
     def stream_voice_clone(self, text, language=None, ref_audio=None, ref_text=None, x_vector_only_mode=False,
-                           voice_clone_prompt=None, non_streaming_mode=False, first_chunk_frames=2, chunk_frames=48,
+                           voice_clone_prompt=None, non_streaming_mode=False, first_chunk_frames=1, chunk_frames=48,
                            **kwargs):
         """New surface (no reference counterpart, SURVEY.md §8f-1 + 8f-2): streaming voice clone.  Same inputs as
         generate_voice_clone (reference audio is encoded / x-vectored at submit); yields (utterance index, pcm chunk
@@ -361,11 +361,12 @@ class Qwen3TTSModel:
 
     @torch.no_grad()
     def stream(self, text, speaker=None, language=None, instruct=None, non_streaming_mode=True,
-               first_chunk_frames=2, chunk_frames=48, left_context=None, **kwargs):
+               first_chunk_frames=1, chunk_frames=48, left_context=None, **kwargs):
         """New surface (no reference counterpart): streaming custom-voice generation.
         Yields (utterance index, pcm chunk np.float32, sample rate, is_last) while the batch decodes: the first
-        chunk arrives after prefill + `first_chunk_frames` decode frames (2 frames: 3285 samples = 0.14 s of audio),
-        later chunks double in size up to `chunk_frames` (each chunk's audio outlasts the generation of the next).  Per utterance the
+        chunk arrives after prefill + `first_chunk_frames` decode frames (1 frame: 1365 samples = 57 ms of audio,
+        which outlasts the ~9 ms the next 2-frame chunk takes), later chunks double in size up to `chunk_frames`
+        (each chunk's audio outlasts the generation of the next).  Per utterance the
         chunks concatenate to the one-shot generate_custom_voice() length and equal its PCM up to fp summation order
         (a stateful incremental codec decode; codes are identical -- see TTSModel.stream for the chunk rule and the
         stateless `left_context` form)."""

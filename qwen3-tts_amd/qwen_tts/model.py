@@ -246,7 +246,7 @@ class TTSModel:
                speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
-               first_chunk_frames=2, chunk_frames=48, left_context=None, use_graph=True, **kwargs):
+               first_chunk_frames=1, chunk_frames=48, left_context=None, use_graph=True, **kwargs):
         """Streaming generation (the reference has none): yields (row, pcm, last) as frames finish.
 
         Per row the chunks concatenate to the one-shot generate() + decode() PCM (Z:259-365): the reference
