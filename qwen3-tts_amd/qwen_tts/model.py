@@ -10,6 +10,7 @@ from typing import Dict, List, Optional
 
 import torch
 
+from . import kernels as K
 from .talker import GenParams, TalkerEngine
 
 
@@ -388,10 +389,23 @@ class TTSModel:
         gpos = 0                          # samples of the (shared) decode timeline produced so far
         scanned = 0                       # cb0 columns already searched for EOS
         k, cs, fed, emit_s, ctx_s = 0, None, 0, 0, 0   # reference chunk, its decoder, positions fed, samples emitted
+        main, side = torch.cuda.current_stream(dev), None
+        if min(R) > 0:
+            # every row starts with reference frames, known at submit: decode them on a side stream while the talker
+            # prefills and generates the first frames on this one
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side), K.use_workspace(K.new_workspace(dev)):
+                cs = dec.stream(B, RX + RC)
+                fed = min(min(R), RC)
+                cs.feed(torch.stack([x[:fed] for x in pre]))
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames, grow=True)
         try:
             for sessions, frames, final in it:
+                if side is not None:
+                    main.wait_stream(side)
+                    side = None
                 # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
                 codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
                 c0 = codes[:, :, 0].cpu()

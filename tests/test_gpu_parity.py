@@ -1216,8 +1216,8 @@ def test_advance_rows_caps_each_row():
     torch.testing.assert_close(c.view(5, B), ref)
 
 
-@pytest.mark.parametrize("frames", [30, 331])
-def test_stream_voice_clone_matches_wrapper(tiny_models, frames):
+@pytest.mark.parametrize("frames,both", [(30, False), (331, False), (30, True)])
+def test_stream_voice_clone_matches_wrapper(tiny_models, frames, both):
     """stream() with a voice-clone prompt (row 0 ICL with 7 reference code frames, row 1 x-vector only): per row the
     chunks concatenate to generate_voice_clone's decode of cat(ref_code, codes) (W:263-274) from the
     reference/generated boundary on, including a > 300-frame sequence whose reference chunk restart falls inside the
@@ -1233,6 +1233,8 @@ def test_stream_voice_clone_matches_wrapper(tiny_models, frames):
     model.load_speech_tokenizer(tok)
     key = "icl_b2"
     case = dict(talker_cases()[key], max_new_tokens=frames)
+    if both:  # every row ICL (7 and 4 reference frames): the common reference prefix is pre-decoded on a side stream
+        case["icl"] = [(5, 7, True, False), (12, 4, True, False)]
     ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
     kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=case["languages"],
               speakers=case["speakers"], non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
