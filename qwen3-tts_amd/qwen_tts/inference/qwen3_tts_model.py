@@ -212,11 +212,14 @@ class Qwen3TTSModel:
             ref_codes = [tok.encode(w, sr=sr).audio_codes[0] for w, sr in normalized]
         items = []
         spk_sr = self.model.speaker_encoder_sample_rate
-        for i, ((wav, sr), code, rtext, xvec_only) in enumerate(zip(normalized, ref_codes, ref_text_list, xvec_list)):
+        for i, (rtext, xvec_only) in enumerate(zip(ref_text_list, xvec_list)):
             if not xvec_only and (rtext is None or rtext == ""):
                 raise ValueError(f"ref_text is required when x_vector_only_mode=False (ICL mode). Bad index={i}")
-            wav_rs = _audio.resample(wav, sr, spk_sr) if sr != spk_sr else wav
-            spk = self.model.extract_speaker_embedding(audio=wav_rs, sr=spk_sr)
+        # x-vectors of all clips (W:434 per clip; equal-length clips share one ECAPA pass here)
+        spks = self.model.extract_speaker_embeddings(
+            [_audio.resample(wav, sr, spk_sr) if sr != spk_sr else wav for wav, sr in normalized], sr=spk_sr)
+        for i, ((wav, sr), code, rtext, xvec_only) in enumerate(zip(normalized, ref_codes, ref_text_list, xvec_list)):
+            spk = spks[i]
             items.append(VoiceClonePromptItem(ref_code=None if xvec_only else code, ref_spk_embedding=spk,
                                               x_vector_only_mode=bool(xvec_only), icl_mode=bool(not xvec_only),
                                               ref_text=rtext))

@@ -73,6 +73,16 @@ class TTSModel:
         with torch.cuda.device(self.device):
             return self.speaker_encoder.embed(audio)
 
+    @torch.inference_mode()
+    def extract_speaker_embeddings(self, audios, sr):
+        """extract_speaker_embedding of several clips at once (equal-length clips share one ECAPA pass):
+        [n][enc_dim] (device, fp32)."""
+        assert sr == 24000, "Only support 24kHz audio"
+        if self.speaker_encoder is None:
+            raise ValueError("no speaker encoder loaded (tts_model_type != 'base', or its weights are absent)")
+        with torch.cuda.device(self.device):
+            return self.speaker_encoder.embed_many(audios)
+
     def get_supported_speakers(self):
         return self.supported_speakers
 

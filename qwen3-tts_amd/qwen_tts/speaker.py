@@ -137,17 +137,15 @@ class SpeakerEncoder:
         torch.cuda.synchronize(dev)
 
     # ------------------------------------------------------------------------------------------------
-    def mel(self, wav: torch.Tensor) -> torch.Tensor:
+    def mel(self, wav: torch.Tensor, check_range: bool = True) -> torch.Tensor:
         """mel_spectrogram (M:405-470) of one fp32 device waveform [L] -> log-mel [frames][128] (time-major)."""
         L = int(wav.shape[0])
         pad = (self.N_FFT - self.HOP) // 2
         if L <= pad:
             raise ValueError(f"reference audio too short for the speaker encoder ({L} samples; reflect padding "
                              f"needs more than {pad})")
-        if float(wav.min()) < -1.0:
-            print(f"[WARNING] Min value of input waveform signal is {float(wav.min())}")
-        if float(wav.max()) > 1.0:
-            print(f"[WARNING] Max value of input waveform signal is {float(wav.max())}")
+        if check_range:
+            self._warn_range([wav])
         Lp = L + 2 * pad
         F_ = (Lp - self.N_FFT) // self.HOP + 1
         rows = -(-Lp // self.HOP)
@@ -215,8 +213,34 @@ class SpeakerEncoder:
         K.gemm(pooled, self.fc, emb, B, 2 * cm, self.fc.N)
         return emb
 
+    @staticmethod
+    def _warn_range(wavs):
+        """mel_spectrogram's range warnings (M:420-423), one host read for all clips."""
+        mm = torch.stack([torch.stack(torch.aminmax(w)) for w in wavs]).cpu()
+        for lo, hi in mm.tolist():
+            if lo < -1.0:
+                print(f"[WARNING] Min value of input waveform signal is {lo}")
+            if hi > 1.0:
+                print(f"[WARNING] Max value of input waveform signal is {hi}")
+
+    def _dev_wav(self, wav) -> torch.Tensor:
+        w = torch.as_tensor(np.asarray(wav, dtype=np.float32) if not isinstance(wav, torch.Tensor) else wav)
+        return w.to(self.dev, torch.float32).reshape(-1)
+
     def embed(self, wav) -> torch.Tensor:
         """extract_speaker_embedding (M:1940-1954): 24 kHz mono waveform -> x-vector fp32 [enc_dim] (device)."""
-        w = torch.as_tensor(np.asarray(wav, dtype=np.float32) if not isinstance(wav, torch.Tensor) else wav)
-        w = w.to(self.dev, torch.float32).reshape(-1)
-        return self.forward(self.mel(w)[None])[0]
+        return self.forward(self.mel(self._dev_wav(wav))[None])[0]
+
+    def embed_many(self, wavs) -> torch.Tensor:
+        """extract_speaker_embedding of several 24 kHz clips -> x-vectors fp32 [n][enc_dim] (device): clips of equal
+        length share one ECAPA pass (rows of one batch; the reference calls it once per clip, W:434)."""
+        ws = [self._dev_wav(w) for w in wavs]
+        self._warn_range(ws)
+        mels = [self.mel(w, check_range=False) for w in ws]
+        out = torch.empty(len(ws), self.fc.N, dtype=torch.float32, device=self.dev)
+        groups = {}
+        for i, m in enumerate(mels):
+            groups.setdefault(m.shape[0], []).append(i)
+        for idx in groups.values():
+            out[idx] = self.forward(torch.stack([mels[i] for i in idx]))
+        return out

@@ -375,3 +375,17 @@ def test_voice_clone_prompt_and_generate(tiny_base):
     assert wc[0].ndim == 1
     with pytest.raises(ValueError):
         tts.create_voice_clone_prompt((w, 24000))  # ICL mode needs ref_text
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_speaker_encoder_batched_clips_match_single(dtype):
+    """embed_many: equal-length clips share one ECAPA pass (rows of one batch), other lengths get their own; every
+    x-vector matches the clip's own embed()."""
+    from cases import ref_audio
+    se = _speaker("tiny-base", dtype)
+    wavs = [ref_audio(24000, 10), ref_audio(24000, 11), ref_audio(30000, 12), ref_audio(24000, 13)]
+    many = se.embed_many(wavs).cpu().numpy()
+    for i, w in enumerate(wavs):
+        one = se.embed(w).cpu().numpy()
+        rel = np.linalg.norm(many[i] - one) / np.linalg.norm(one)
+        assert rel < (1e-5 if dtype == "fp32" else 2e-2), (i, rel)
