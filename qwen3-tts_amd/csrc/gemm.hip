@@ -643,6 +643,160 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
   }
 }
 
+// Prefill linear GEMM (taps == 0, bf16 pre-tiled weights, M >= 128 rows): block tile 128 rows x NTB*16 columns,
+// 4 waves in a 2 x 2 grid (wave = 64 rows x NTB/2 column tiles of 16x16x32 MFMAs), K in 64-wide stages.  Both
+// operands are staged through LDS and double-buffered: the next stage's global loads (A rows fp32/bf16 -> bf16 with
+// the RMS sums of squares taken on the way, B as the pre-tiled 1 KiB fragments, copied verbatim) are in flight
+// while the current stage is multiplied, one barrier per stage.  igemm_k streamed B straight from L2 one k tile
+// ahead, which left every MFMA group waiting on an L2 round trip (tools/prefill_gemm_bench.py: M=680 gate-up
+// 106.8 us = 320 TFLOP/s).  Same operand rounding and per-element k order as igemm_k.
+constexpr int PF_BM = 128, PF_BK = 64, PF_AST = PF_BK + 8;  // A LDS row stride (bf16): 144 B
+
+template <typename AT, typename OT, int NTB>
+__global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
+  constexpr int CT = NTB / 2;                 // column tiles per wave
+  constexpr int BT = NTB * 2;                 // B fragments (1 KiB) per stage
+  constexpr int BPT = BT * 64 / 256;          // 16-byte B loads per thread per stage
+  constexpr int AE = sizeof(AT) == 4 ? 8 : 4; // 16-byte A loads per thread per stage (32 elements)
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][PF_BM * PF_AST];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BT * 512];
+  __shared__ float ss_row[PF_BM];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lm = lane & 15, lk = lane >> 4;
+  const int m0 = blockIdx.x * PF_BM, nt0 = blockIdx.y * NTB;
+  const int ntl = (p.N + 15) / 16, ktiles = p.Kp / 32, S = (ktiles + 1) / 2;
+  const int wr = (w >> 1) * 64, wc = (w & 1) * CT;
+  const bool norm = p.rms != 0;
+  // A staging: thread -> row ar (0..127), k half ah (32 elements)
+  const int ar = tid >> 1, ah = tid & 1;
+  const bool arow = m0 + ar < p.M;
+  const AT* Ar = (const AT*)p.A + (long long)(arow ? m0 + ar : 0) * p.lda;
+  float sst = 0.f;
+  u32x4_t ra[AE], rb[BPT];
+  auto load_stage = [&](int st) {
+    const int k0 = st * PF_BK + ah * 32;
+#pragma unroll
+    for (int i = 0; i < AE; ++i) {
+      const int k = k0 + i * (32 / AE);
+      ra[i] = (arow && k < p.Klog) ? *(const u32x4_t*)(Ar + k) : u32x4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int q = tid + i * 256, ti = q >> 6;      // fragment ti of the stage: column tile ti >> 1, k tile ti & 1
+      const int nt = min(nt0 + (ti >> 1), ntl - 1), kt = st * 2 + (ti & 1);
+      const bf16_t* src = (const bf16_t*)p.W + ((size_t)nt * ktiles + min(kt, ktiles - 1)) * 512 + (q & 63) * 8;
+      rb[i] = kt < ktiles ? *(const u32x4_t*)src : u32x4_t{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_stage = [&](int buf) {
+    bf16_t* ad = As[buf] + ar * PF_AST + ah * 32;
+    if constexpr (sizeof(AT) == 4) {
+#pragma unroll
+      for (int i = 0; i < AE; i += 2) {  // two 16-byte fp32 loads -> one 16-byte bf16 store
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] = __uint_as_float(ra[i][e]); v[4 + e] = __uint_as_float(ra[i + 1][e]); }
+        if (norm) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sst += v[e] * v[e];
+        }
+        *(u32x4_t*)(ad + i * 4) =
+            u32x4_t{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AE; ++i) {
+        if (norm) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = __uint_as_float(ra[i][e] << 16), hi = __uint_as_float(ra[i][e] & 0xFFFF0000u);
+            sst += lo * lo + hi * hi;
+          }
+        }
+        *(u32x4_t*)(ad + i * 8) = ra[i];
+      }
+    }
+    bf16_t* bd = Bs[buf];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) *(u32x4_t*)(bd + (size_t)(tid + i * 256) * 8) = rb[i];
+  };
+  f32x4_t acc[4][CT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  for (int st = 0; st < S; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < S) load_stage(st + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4_t af[4], bf[CT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const u32x4_t*)(As[buf] + (wr + i * 16 + lm) * PF_AST + kk * 32 + lk * 8);
+#pragma unroll
+      for (int j = 0; j < CT; ++j) bf[j] = *(const u32x4_t*)(Bs[buf] + ((wc + j) * 2 + kk) * 512 + lane * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                              __builtin_bit_cast(bf16x8_t, bf[j]), acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < S) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+  if (norm) {
+    const float s2 = sst + __shfl_xor(sst, 1, 64);
+    if (ah == 0) ss_row[ar] = s2;
+    __syncthreads();
+  }
+  OT* out = (OT*)p.out;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int q = 0; q < CT; ++q) {
+      const int nt = nt0 + wc + q;
+      if (nt >= ntl) continue;
+      const int n = nt * 16 + lm;
+      const bool nval = n < p.N;
+      const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
+      const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rl = wr + i * 16 + lk * 4 + e;
+        float x = acc[i][q][e];
+        if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
+        x += bias;
+        if (p.act != QT_ACT_NONE) x = act_f_call(x, p.act);
+        v[e] = x * cs;
+      }
+      if (p.epi == QT_EPI_SWIGLU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float up = __shfl_xor(v[e], 8, 64);
+          const int m = m0 + wr + i * 16 + lk * 4 + e;
+          if (lm < 8 && m < p.M && nt * 8 + lm < (p.N >> 1))
+            out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[e]) * up);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wr + i * 16 + lk * 4 + e;
+        if (m >= p.M || !nval) continue;
+        OT* o = out + (long long)m * p.ldo + n;
+        const float r = p.epi == QT_EPI_ADD ? to_f(*o) + v[e] : v[e];
+        *o = from_f<OT>(r);
+        if (p.out2) p.out2[(long long)m * p.ldo2 + n] = f2bf(r);
+      }
+    }
+  }
+}
+
 // Single-output-channel causal conv (codec conv_last, Cout = 1): memory-bound, so no MFMA.  A block owns
 // 256 consecutive outputs of one batch item; the input window (256 + (taps-1)*dil rows) x 32 channels is staged
 // in LDS per channel chunk (SnakeBeta applied on staging) and each thread accumulates its output's taps x cin
@@ -784,6 +938,26 @@ inline int igemm_min_m() {
   return v;
 }
 
+// the LDS-staged prefill GEMM (gemm_pf_k) for taps == 0 linears; QT_PF=0 keeps them on igemm_k (measurement)
+inline bool pf_on() {
+  static const bool v = [] { const char* e = getenv("QT_PF"); return e ? atoi(e) != 0 : true; }();
+  return v;
+}
+// widest output served by gemm_pf_k (QT_PF_NMAX, measurement; 0 = any)
+inline int pf_nmax() {
+  static const int v = [] { const char* e = getenv("QT_PF_NMAX"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
+// gemm_pf_k serves bf16-A linears (the bf16 residual shadow, attention / SwiGLU outputs); with fp32 A its 32 KiB
+// per-stage A fetch from beyond L2 is not hidden by one stage of prefetch (M=680 gate-up 184 vs 107 us on igemm_k)
+template <typename WT, typename AT>
+bool pf_route(const GemmP& p) {
+  return sizeof(WT) == 2 && sizeof(AT) == 2 && p.taps == 0 && pf_on() && p.a_index == nullptr && p.gamma == nullptr &&
+         p.N >= 32 && (pf_nmax() == 0 || p.N <= pf_nmax()) && p.M >= igemm_min_m() && p.mr > 16 && p.Klog % 8 == 0 && p.lda % 8 == 0 && !p.a_elu &&
+         p.sn_a == nullptr && !p.no_igemm;
+}
+
 template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
@@ -802,6 +976,12 @@ int launch(const GemmP& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_n1_k<AT, WT, OT>), dim3(batches * ((p.t_out + 255) / 256)), dim3(256), smem, s, p);
   } else if (p.M <= 16) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
+  } else if (pf_route<WT, AT>(p)) {
+    // prefill linears: LDS-staged A and B, 128 x 128 tiles (128 x 64 when that leaves < 256 blocks)
+    const int mt = (p.M + PF_BM - 1) / PF_BM;
+    const bool narrow = (long long)mt * ((nt + 7) / 8) < 256;
+    if (narrow) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
   } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 &&
              p.M >= (p.taps > 0 ? 16 : igemm_min_m()) &&
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
@@ -950,10 +1130,14 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
     p.ks = 1;
     if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
   }
-  // out2 is written by the decode GEMV's epilogue only (M <= 16, or the skinny row-group path above)
-  if (p.out2 && (p.mr > 16 || a->K % KT != 0 || a->gamma != nullptr || a->a_act != QT_AACT_NONE)) return QT_ERR_ARG;
+  const int w = a->w_dtype, o = a->o_dtype;
+  // out2 is written by the decode GEMV's epilogue (M <= 16, or the skinny row-group path above) and by gemm_pf_k
+  // (bf16-A prefill linears)
+  const bool pf = w == QT_BF16 && a->a_dtype == QT_BF16 && pf_route<bf16_t, bf16_t>(p);
+  if (p.out2 && !pf && (p.mr > 16 || a->K % KT != 0 || a->gamma != nullptr || a->a_act != QT_AACT_NONE))
+    return QT_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int w = a->w_dtype, ad = a->a_dtype, o = a->o_dtype;
+  const int ad = a->a_dtype;
   if (w == QT_BF16 && ad == QT_F32 && o == QT_F32) return launch<bf16_t, float, float>(p, s);
   if (w == QT_BF16 && ad == QT_BF16 && o == QT_BF16) return launch<bf16_t, bf16_t, bf16_t>(p, s);
   if (w == QT_BF16 && ad == QT_BF16 && o == QT_F32) return launch<bf16_t, bf16_t, float>(p, s);

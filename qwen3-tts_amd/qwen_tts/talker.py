@@ -86,8 +86,8 @@ class _Stack:
         and the next RMS GEMV (next layer's q/k/v, or the head W into out) as one persistent qt_cp_mlp launch."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
-        if x16 is not None and ("mlp_ws" in scratch or R > 96):
-            x16 = None  # the fused MLP / large-M prefill GEMMs write x only (decode / skinny GEMVs keep the shadow)
+        if x16 is not None and ("mlp_ws" in scratch or (R > 96 and not PF)):
+            x16 = None  # the fused MLP / igemm_k write x only (decode / skinny GEMVs and gemm_pf_k keep the shadow)
         xa = x if x16 is None else x16
         use_mlp = mlp is not None and fused_ao and x16 is not None and R <= 16
         for li, L in enumerate(self.layers):
@@ -141,6 +141,9 @@ CP_MLP = os.environ.get("QT_CP_MLP", "0") == "1"
 # talker prefill captured into a HIP graph per (session, prompt length) once that length repeats; QT_PREFILL_GRAPH=0
 # always issues it eagerly (A/B)
 PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
+# large-M prefill linears on gemm_pf_k (LDS-staged bf16 A and B): the prefill keeps the bf16 residual shadow at any
+# row count, so its RMS GEMMs read bf16 A too; QT_PF=0 (read by the library as well) keeps igemm_k (A/B)
+PF = os.environ.get("QT_PF", "1") != "0"
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -774,7 +777,7 @@ class TalkerEngine:
                    "meta": {"rope_pos": ar, "kv_pos": ar.clone(), "row_len": ar + 1, "row_start": i32(P),
                             "row_batch": i32(P)},
                    "x16": (torch.empty(P, H, dtype=torch.bfloat16, device=dev)
-                           if X16 and self.wdt == torch.bfloat16 and P <= 96 else None)}
+                           if X16 and self.wdt == torch.bfloat16 and (P <= 96 or PF) else None)}
             s.slot_prefill[P] = pre
         pre["meta"]["row_batch"].fill_(b)
         pre["x"].copy_(emb.reshape(P, H))
@@ -822,7 +825,7 @@ class TalkerEngine:
                    "last": torch.empty(B, H, dtype=torch.float32, device=dev), "graph": None, "uses": 0,
                    # bf16 shadow of the prefill residual (skinny-GEMV row counts): the RMS GEMVs read half the bytes
                    "x16": (torch.empty(R, H, dtype=torch.bfloat16, device=dev)
-                           if X16 and self.wdt == torch.bfloat16 and R <= 96 else None)}
+                           if X16 and self.wdt == torch.bfloat16 and (R <= 96 or PF) else None)}
             s.prefill[P] = pre
         pre["meta"]["rope_pos"].copy_(pos.reshape(-1))
         pre["meta"]["row_start"].copy_(torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])

@@ -229,13 +229,13 @@ def test_igemm_transposed_conv_bf16(s):
     torch.testing.assert_close(out.view(B, (T - 1) * s, cout).permute(0, 2, 1).cpu(), ref, atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("M", [128, 300])
-def test_igemm_linear_rms_swiglu_bf16(M):
-    """Large-M linears on the tiled path: folded-gamma RMSNorm rows, SwiGLU epilogue, residual add."""
+@pytest.mark.parametrize("M,H,I", [(128, 256, 384), (300, 256, 384), (700, 288, 400), (1100, 512, 1024)])
+def test_igemm_linear_rms_swiglu_bf16(M, H, I):
+    """Large-M linears on the tiled path (gemm_pf_k: 128 x 128 / 128 x 64 tiles, ragged row / column / k tiles):
+    folded-gamma RMSNorm rows, SwiGLU epilogue, residual add."""
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
     g = torch.Generator().manual_seed(M)
-    H, I = 256, 384
     x = torch.randn(M, H, generator=g)
     gamma = 1 + 0.1 * torch.randn(H, generator=g)
     gate, up = torch.randn(I, H, generator=g) * 0.05, torch.randn(I, H, generator=g) * 0.05

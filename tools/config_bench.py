@@ -110,11 +110,21 @@ def config4(reps, B=4):
 
     fp, _ = timed(first, reps)
     enc, _ = timed(prompt, reps)
+    # first-packet breakdown: prompt assembly (ICL layout), prefill + first frame, codec decode of the reference
+    # frames + one generated frame
+    vcp = prompt()
+    asm, _ = timed(lambda: m.build_prompts(ids, ["english"] * B, None, None, False, vcp, ref_ids), reps)
+    g1, _ = timed(lambda: m.generate(input_ids=ids, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=["english"] * B,
+                                     non_streaming_mode=False, **dict(gen, max_new_tokens=2)), reps)
+    dec = m.speech_tokenizer.model
+    cc = torch.randint(1, 2048, (B, R + 1, 16), device="cuda", dtype=torch.int32)
+    cf, _ = timed(lambda: dec.stream(B, 325).feed(cc), reps)
     return {"config": f"configs[4] 1.7B-Base voice clone, {B} requests per GPU (32 over 8 GPUs): 3 s reference clips "
                       f"({R} ref frames, ICL) encode + x-vector, 120-token text, {F} frames sampled + codec",
             "latency_ms": round(1e3 * dt, 1), "audio_s": round(audio, 3), "audio_s_per_s": round(audio / dt, 2),
             "rtf_per_utterance": round(audio / dt / B, 2), "first_packet_p50_ms": round(1e3 * fp, 1),
-            "voice_clone_prompt_ms": round(1e3 * enc, 2)}
+            "voice_clone_prompt_ms": round(1e3 * enc, 2), "prompt_assembly_ms": round(1e3 * asm, 2),
+            "generate_1_frame_ms": round(1e3 * g1, 2), "codec_ref_plus_1_frame_ms": round(1e3 * cf, 2)}
 
 
 def main():

@@ -13,8 +13,10 @@ dev = torch.device("cuda:0")
 
 
 def main():
-    shapes = [("qkv", 4096, 2048, True, 0, torch.float32), ("o", 2048, 2048, False, 1, torch.bfloat16),
-              ("gate-up", 12288, 2048, True, 2, torch.float32), ("down", 2048, 6144, False, 1, torch.bfloat16)]
+    # the RMS GEMMs read the bf16 residual shadow when the prefill runs on gemm_pf_k (QT_PF != 0), else fp32 x
+    xdt = torch.float32 if os.environ.get("QT_PF", "1") == "0" else torch.bfloat16
+    shapes = [("qkv", 4096, 2048, True, 0, xdt), ("o", 2048, 2048, False, 1, torch.bfloat16),
+              ("gate-up", 12288, 2048, True, 2, xdt), ("down", 2048, 6144, False, 1, torch.bfloat16)]
     for M in [int(m) for m in os.environ.get("QT_PB_M", "24,48,80,112,160,256").split(",")]:
         for name, N, Kk, rms, epi, adt in shapes:
             nmat = max(2, int(600e6 // (N * Kk * 2)))
