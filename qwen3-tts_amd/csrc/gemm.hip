@@ -943,6 +943,11 @@ inline bool pf_on() {
   static const bool v = [] { const char* e = getenv("QT_PF"); return e ? atoi(e) != 0 : true; }();
   return v;
 }
+// fewest rows served by gemm_pf_k (QT_PF_MIN_M, measurement; default the igemm_k threshold)
+inline int pf_min_m() {
+  static const int v = [] { const char* e = getenv("QT_PF_MIN_M"); return e ? atoi(e) : 0; }();
+  return v;
+}
 // widest output served by gemm_pf_k (QT_PF_NMAX, measurement; 0 = any)
 inline int pf_nmax() {
   static const int v = [] { const char* e = getenv("QT_PF_NMAX"); return e ? atoi(e) : 0; }();
@@ -954,7 +959,7 @@ inline int pf_nmax() {
 template <typename WT, typename AT>
 bool pf_route(const GemmP& p) {
   return sizeof(WT) == 2 && sizeof(AT) == 2 && p.taps == 0 && pf_on() && p.a_index == nullptr && p.gamma == nullptr &&
-         p.N >= 32 && (pf_nmax() == 0 || p.N <= pf_nmax()) && p.M >= igemm_min_m() && p.mr > 16 && p.Klog % 8 == 0 && p.lda % 8 == 0 && !p.a_elu &&
+         p.N >= 32 && (pf_nmax() == 0 || p.N <= pf_nmax()) && p.M >= std::max(igemm_min_m(), pf_min_m()) && p.mr > 16 && p.Klog % 8 == 0 && p.lda % 8 == 0 && !p.a_elu &&
          p.sn_a == nullptr && !p.no_igemm;
 }
 
