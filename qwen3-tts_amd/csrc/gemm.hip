@@ -652,7 +652,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
 // 106.8 us = 320 TFLOP/s).  Same operand rounding and per-element k order as igemm_k.
 constexpr int PF_BM = 128, PF_BK = 64, PF_AST = PF_BK + 8;  // A LDS row stride (bf16): 144 B
 
-template <typename AT, typename OT, int NTB>
+template <typename AT, typename OT, int NTB, bool P2>
 __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   constexpr int CT = NTB / 2;                 // column tiles per wave
   constexpr int BT = NTB * 2;                 // B fragments (1 KiB) per stage
@@ -673,7 +673,8 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   const AT* Ar = (const AT*)p.A + (long long)(arow ? m0 + ar : 0) * p.lda;
   float sst = 0.f;
   u32x4_t ra[AE], rb[BPT];
-  auto load_stage = [&](int st) {
+  u32x4_t ra2[P2 ? AE : 1], rb2[P2 ? BPT : 1];  // second register set: two stages of loads in flight (P2)
+  auto load_stage = [&](int st, u32x4_t* ra, u32x4_t* rb) {
     const int k0 = st * PF_BK + ah * 32;
 #pragma unroll
     for (int i = 0; i < AE; ++i) {
@@ -688,7 +689,7 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
       rb[i] = kt < ktiles ? *(const u32x4_t*)src : u32x4_t{0u, 0u, 0u, 0u};
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, const u32x4_t* ra, const u32x4_t* rb) {
     bf16_t* ad = As[buf] + ar * PF_AST + ah * 32;
     if constexpr (sizeof(AT) == 4) {
 #pragma unroll
@@ -725,12 +726,7 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-  for (int st = 0; st < S; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < S) load_stage(st + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       u32x4_t af[4], bf[CT];
@@ -745,8 +741,35 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
                                                               __builtin_bit_cast(bf16x8_t, bf[j]), acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < S) store_stage(buf ^ 1);
+  };
+  load_stage(0, ra, rb);
+  if constexpr (P2) {
+    // stage s is multiplied from LDS buffer s & 1 while stage s + 1 waits in one register set and stage s + 2 is
+    // loaded into the other: two stages of global latency hidden instead of one
+    if (S > 1) load_stage(1, ra2, rb2);
+    store_stage(0, ra, rb);
     __syncthreads();
+    for (int st = 0; st < S; st += 2) {
+      if (st + 2 < S) load_stage(st + 2, ra, rb);
+      compute(0);
+      if (st + 1 < S) store_stage(1, ra2, rb2);
+      __syncthreads();
+      if (st + 1 >= S) break;
+      if (st + 3 < S) load_stage(st + 3, ra2, rb2);
+      compute(1);
+      if (st + 2 < S) store_stage(0, ra, rb);
+      __syncthreads();
+    }
+  } else {
+    store_stage(0, ra, rb);
+    __syncthreads();
+    for (int st = 0; st < S; ++st) {
+      const int buf = st & 1;
+      if (st + 1 < S) load_stage(st + 1, ra, rb);
+      compute(buf);
+      if (st + 1 < S) store_stage(buf ^ 1, ra, rb);
+      __syncthreads();
+    }
   }
   if (norm) {
     const float s2 = sst + __shfl_xor(sst, 1, 64);
@@ -985,8 +1008,11 @@ int launch(const GemmP& p, hipStream_t s) {
     // prefill linears: LDS-staged A and B, 128 x 128 tiles (128 x 64 when that leaves < 256 blocks)
     const int mt = (p.M + PF_BM - 1) / PF_BM;
     const bool narrow = (long long)mt * ((nt + 7) / 8) < 256;
-    if (narrow) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
+    static const bool p2 = [] { const char* e = getenv("QT_PF_P2"); return e ? atoi(e) != 0 : false; }();
+    if (narrow && p2) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4, true>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
+    else if (narrow) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4, false>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
+    else if (p2) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8, true>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8, false>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
   } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 &&
              p.M >= (p.taps > 0 ? 16 : igemm_min_m()) &&
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
