@@ -72,6 +72,13 @@ def synth_param(name: str, shape, seed: int = 1234) -> np.ndarray:
     return (0.02 * n()).astype(np.float32)
 
 
-def synth_state_dict(specs, seed: int = 1234):
-    """specs: iterable of (name, shape) -> {name: np.float32 array}."""
+def synth_state_dict(specs, seed: int = 1234, threads: int = 0):
+    """specs: iterable of (name, shape) -> {name: np.float32 array}.  threads > 0 draws the parameters on a thread
+    pool (each has its own generator, so the values do not depend on the order or the pool size)."""
+    specs = list(specs)
+    if threads > 0:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(threads) as ex:
+            vals = list(ex.map(lambda ns: synth_param(ns[0], ns[1], seed), specs))
+        return {name: v for (name, _), v in zip(specs, vals)}
     return {name: synth_param(name, shape, seed) for name, shape in specs}

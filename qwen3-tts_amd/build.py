@@ -1,13 +1,17 @@
 """Build libqwen3tts_amd.so (all HIP kernels + the C ABI of include/qwen3tts_amd.h) for gfx950.
 
-    python qwen3-tts_amd/build.py [--jobs N]
+    python qwen3-tts_amd/build.py [--jobs N] [--force]
 
 Plain hipcc, one object per .hip source (parallel), linked into lib/libqwen3tts_amd.so in-tree so the
-library travels with the repo snapshot to the GPU box.  Rebuilds only stale objects.
+library travels with the repo snapshot to the GPU box.  Staleness is decided by content, not mtime: every
+object records the digest of its source + the shared headers + the flags, and the library carries the digest
+of the whole source set as `qt_build_id()` (a generated one-line source), which `qwen_tts._hip` compares with
+the sources next to it at load time -- a library that does not match the tree it ships with is refused.
 """
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -20,40 +24,85 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-munsafe-fp-atomics"]
 
 
-def _deps():
-    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(HERE, "..", "include", "*.h"))
-    return max((os.path.getmtime(h) for h in hdrs), default=0)
+def _read(p):
+    with open(p, "rb") as f:
+        return f.read()
 
 
-def _compile(src):
+def _headers():
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(HERE, "..", "include", "*.h")))
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def source_digest(csrc=CSRC) -> str:
+    """sha256 over every kernel source, the shared headers and the compile flags (16 hex digits)."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    inc = os.path.join(os.path.dirname(csrc), "..", "include")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))
+                   + glob.glob(os.path.join(inc, "*.h")))
+    for p in files:
+        h.update(os.path.basename(p).encode())
+        h.update(_read(p))
+    return h.hexdigest()[:16]
+
+
+def _obj_digest(src):
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in [src] + _headers():
+        h.update(_read(p))
+    return h.hexdigest()
+
+
+def _compile(src, force=False):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), _deps()):
+    stamp = obj + ".sha"
+    dig = _obj_digest(src)
+    if not force and os.path.exists(obj) and os.path.exists(stamp) and _read(stamp).decode() == dig:
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(dig)
     return obj
 
 
-def build(jobs=8, verbose=True):
+def _build_id_obj(bid):
+    src = os.path.join(BUILD, "build_id.hip")
+    with open(src, "w") as f:
+        f.write(f'extern "C" const char* qt_build_id() {{ return "{bid}"; }}\n')
+    return _compile(src)
+
+
+def build(jobs=8, verbose=True, force=False):
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    bid = source_digest()
+    objs.append(_build_id_obj(bid))
+    stamp = LIB + ".sha"
+    link_key = bid + " " + " ".join(sorted(os.path.basename(o) for o in objs))
+    if force or not os.path.exists(LIB) or not os.path.exists(stamp) or _read(stamp).decode() != link_key:
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        with open(stamp, "w") as f:
+            f.write(link_key)
     if verbose:
-        print(f"built {LIB}")
+        print(f"built {LIB} (build id {bid})")
     return LIB
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--force", action="store_true")
     a = ap.parse_args()
-    sys.exit(0 if build(a.jobs) else 1)
+    sys.exit(0 if build(a.jobs, force=a.force) else 1)

@@ -547,6 +547,11 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     }  // !fast
   }
   if (finv) tok = p.eos_id;
+  if (p.force) {  // teacher forcing: record this path's choice, continue with the forced token
+    const long long off = (long long)r * p.codes_ld + (long long)((int)stp + p.codes_step_off) * p.codes_w + p.codes_col;
+    if (tid == 0) p.pick[off] = tok;
+    tok = p.force[off];
+  }
   if (pk.stop == 5) {
     if (tid == 0) p.tok_out[r] = tok;
     return;
@@ -597,6 +602,7 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (a->emb_table && (!a->emb_out || a->emb_dim % 4 || a->emb_ld % 4)) return QT_ERR_SHAPE;
   if (a->emb_out16 && (!a->emb_table || a->emb_ld16 % 4)) return QT_ERR_SHAPE;
   if (a->emb2_table && (!a->emb_table || !a->emb2_out || a->emb2_dim % 4 || a->emb2_ld % 4)) return QT_ERR_SHAPE;
+  if (a->force && (!a->pick || !a->codes)) return QT_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
   const SK k{*a, stop};

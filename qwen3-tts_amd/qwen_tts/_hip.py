@@ -80,38 +80,52 @@ class SampleArgs(ctypes.Structure):
                 ("emb_table", c_void_p), ("emb_dim", c_int), ("emb_out", c_void_p), ("emb_ld", c_ll),
                 ("seed_ptr", c_void_p), ("debug_u", c_float), ("emb_out16", c_void_p), ("emb_ld16", c_ll),
                 ("emb2_table", c_void_p), ("emb2_dim", c_int), ("emb2_out", c_void_p), ("emb2_ld", c_ll),
-                ("algo", c_int), ("ctr_stride", c_int), ("philox_row", c_void_p)]
-
-
-class MlpArgs(ctypes.Structure):
-    _fields_ = [("M", c_int), ("H", c_int), ("I", c_int), ("x", c_void_p), ("ldx", c_ll), ("w_gu", c_void_p),
-                ("w_down", c_void_p), ("eps", c_float), ("ws", c_void_p), ("ws_bytes", c_ll), ("err", c_void_p)]
-
-
-class CpMlpArgs(ctypes.Structure):
-    _fields_ = [("M", c_int), ("H", c_int), ("I", c_int), ("N3", c_int), ("x16", c_void_p), ("ldx16", c_ll),
-                ("x", c_void_p), ("ldx", c_ll), ("w_gu", c_void_p), ("w_down", c_void_p), ("w3", c_void_p),
-                ("eps", c_float), ("out3", c_void_p), ("ldo3", c_ll), ("tags", c_void_p), ("tags_bytes", c_ll),
-                ("epoch_ctr", c_void_p), ("epoch_mul", c_int), ("epoch_add", c_int), ("err", c_void_p)]
+                ("algo", c_int), ("ctr_stride", c_int), ("philox_row", c_void_p), ("force", c_void_p),
+                ("pick", c_void_p)]
 
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
-           "qt_mlp_ws_bytes", "qt_rmsnorm_rec", "qt_small_prefill_attention",
+           "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj",
-           "qt_mlp_decode", "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
+           "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
-           "qt_scale_add", "qt_bcast_rows", "qt_cp_mlp", "qt_cp_mlp_tags_bytes", "qt_cp_mlp_supported"]
+           "qt_scale_add", "qt_bcast_rows", "qt_build_id"]
 
 _LIB = None
+BUILD_ID = None  # qt_build_id() of the loaded library (digest of the sources it was built from)
+
+
+def source_digest():
+    """Digest of the kernel sources shipped next to this package (qwen3-tts_amd/build.py's source_digest), or
+    None when they are absent (an installed copy without sources)."""
+    bpath = os.path.join(os.path.dirname(HERE), "build.py")
+    if not os.path.exists(bpath) or not os.path.isdir(os.path.join(os.path.dirname(HERE), "csrc")):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_qt_build", bpath)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_digest()
 
 
 def load_library(path: str = LIB_PATH):
-    """dlopen the library and declare signatures (no GPU needed; used by the CPU export test)."""
+    """dlopen the library and declare signatures (no GPU needed; used by the CPU export test).  A library whose
+    qt_build_id() differs from the digest of the kernel sources beside it is stale and refused (set
+    QT_ALLOW_STALE_LIB=1 to load it anyway, e.g. for an A/B of an older build)."""
     if not os.path.exists(path):
         raise RuntimeError(f"HIP library not found at {path}: run `python qwen3-tts_amd/build.py` "
                            "(or __graft_entry__.build()); there is no CPU fallback")
     L = ctypes.CDLL(path)
+    L.qt_build_id.restype = ctypes.c_char_p
+    L.qt_build_id.argtypes = []
+    bid = L.qt_build_id().decode()
+    want = source_digest() if path == LIB_PATH else None
+    if want is not None and bid != want and os.environ.get("QT_ALLOW_STALE_LIB") != "1":
+        raise RuntimeError(f"{path} was built from other sources (build id {bid}, sources {want}): rebuild with "
+                           "`python qwen3-tts_amd/build.py`")
+    global BUILD_ID
+    BUILD_ID = bid
     P = c_void_p
     sig = {
         "qt_gemm": [P, P], "qt_tile_weight": [P, c_int, c_int, c_int, P, P], "qt_qkv_post": [P, P],
@@ -126,10 +140,9 @@ def load_library(path: str = LIB_PATH):
         "qt_rvq_gather": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P],
         "qt_snake": [P, P, c_int, c_ll, c_int, P, P, P],
         "qt_dwconv_ln": [P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P],
-        "qt_clamp_pcm": [P, c_int, c_ll, P, P], "qt_mlp_decode": [P, P], "qt_mlp_ws_bytes": [c_int, c_int, c_int],
+        "qt_clamp_pcm": [P, c_int, c_ll, P, P],
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
         "qt_decode_attn_oproj": [P, P],
-        "qt_cp_mlp": [P, P], "qt_cp_mlp_tags_bytes": [c_int, c_int], "qt_cp_mlp_supported": [c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],
@@ -143,7 +156,7 @@ def load_library(path: str = LIB_PATH):
     for name, args in sig.items():
         f = getattr(L, name)
         f.argtypes = args
-        f.restype = c_ll if name.endswith("_ws_bytes") or name.endswith("_tags_bytes") else c_int
+        f.restype = c_ll if name.endswith("_ws_bytes") else c_int
     return L
 
 
@@ -154,6 +167,17 @@ def lib():
             raise RuntimeError("qwen_tts (MI355X build) needs a ROCm GPU: no device visible and no CPU fallback")
         _LIB = load_library()
     return _LIB
+
+
+def env_int(name: str, default: int) -> int:
+    """An integer environment knob parsed like C atoi (as the library's own getenv knobs are): optional leading
+    whitespace and sign, then digits; anything else (empty, 'off') is 0.  Unset -> default."""
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    import re
+    m = re.match(r"\s*([+-]?\d+)", v)
+    return int(m.group(1)) if m else 0
 
 
 def check(rc: int, what: str):

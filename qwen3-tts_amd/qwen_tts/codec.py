@@ -260,6 +260,9 @@ class _StreamSlot:
         self.graphs = {}    # (n, first) -> (graph, static codes input, static pcm output)
         self.uses = {}
         self.busy = False
+        # split-K scratch of this slot's GEMVs: every feed of the slot (eager or captured) uses it, whatever stream
+        # or workspace context the caller is in, so a captured feed graph never points at a caller's temporary
+        self.ws = K.new_workspace(dev)
 
     def reset(self):
         for h in self.hist.values():
@@ -288,7 +291,8 @@ class CodecStream:
     def __init__(self, dec: "CodecDecoder", B: int, max_frames: int):
         self.dec, self.B, self.max_frames = dec, B, max_frames
         d = dec.d
-        if dec.cos.shape[0] < max_frames:
+        if dec.cos.shape[0] < max_frames:  # old tables stay alive: other slots' captured feed graphs read them
+            dec._old_rope = getattr(dec, "_old_rope", []) + [(dec.cos, dec.sin)]
             dec.cos, dec.sin = K.rope_tables(dec.hd, d["rope_theta"], max_frames + 64, dec.dev)
         self.slot = dec._acquire_slot(B, max_frames)
         self.nf = 0  # frames fed
@@ -442,10 +446,11 @@ class CodecStream:
             g[0].replay()
             pcm = g[2]
         else:
-            pcm = self._compute(codes, n, key[1])
-            slot.uses[key] = slot.uses.get(key, 0) + 1
-            if CODEC_GRAPH and slot.uses[key] >= 2:
-                slot.graphs[key] = self._capture(codes, n, key[1])
+            with K.use_workspace(slot.ws):
+                pcm = self._compute(codes, n, key[1])
+                slot.uses[key] = slot.uses.get(key, 0) + 1
+                if CODEC_GRAPH and slot.uses[key] >= 2:
+                    slot.graphs[key] = self._capture(codes, n, key[1])
         self.nf += n
         L = pcm.shape[1]
         self.pcm[:, self.ns:self.ns + L] = pcm

@@ -286,6 +286,10 @@ class Qwen3TTSModel:
             if ref_audio is None:
                 raise ValueError("Either `voice_clone_prompt` or `ref_audio` must be provided.")
             items = self.create_voice_clone_prompt(ref_audio, ref_text, x_vector_only_mode)
+            if len(items) == 1 and len(texts) > 1:  # one reference voice for a batch of texts (W:567-571)
+                items = items * len(texts)
+            if len(items) != len(texts):
+                raise ValueError(f"Batch size mismatch: prompt={len(items)}, text={len(texts)}")
             vcp, ref_texts = self._prompt_items_to_voice_clone_prompt(items), [it.ref_text for it in items]
         elif isinstance(voice_clone_prompt, list):
             items = voice_clone_prompt

@@ -169,46 +169,6 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     check(_hip.lib().qt_gemm(ctypes.byref(a), stream()), "qt_gemm")
 
 
-def mlp_ws_bytes(M, H, I):
-    return int(_hip.lib().qt_mlp_ws_bytes(M, H, I))
-
-
-def mlp_supported(H, I, wdt) -> bool:
-    return wdt == torch.bfloat16 and H in (1024, 2048) and I % 32 == 0 and H // 16 <= I // 32 <= 256
-
-
-def mlp_decode(x, M, H, I, w_gu: "Tiled", w_down: "Tiled", eps, ws, err=None):
-    """Fused decode MLP + residual (qt_mlp_decode): x[:M] += down(SwiGLU(rms(x) gate/up)); x fp32 [M][H]."""
-    a = _hip.MlpArgs()
-    a.M, a.H, a.I, a.x, a.ldx = M, H, I, ptr(x), x.stride(0)
-    a.w_gu, a.w_down, a.eps = ptr(w_gu.w), ptr(w_down.w), eps
-    a.ws, a.ws_bytes, a.err = ptr(ws), ws.numel() * ws.element_size(), ptr(err)
-    check(_hip.lib().qt_mlp_decode(ctypes.byref(a), stream()), "qt_mlp_decode")
-
-
-def cp_mlp_tags_bytes(H, I):
-    return int(_hip.lib().qt_cp_mlp_tags_bytes(H, I))
-
-
-def cp_mlp_supported(M, H, I, N3) -> bool:
-    return bool(_hip.lib().qt_cp_mlp_supported(M, H, I, N3))
-
-
-def cp_mlp(x16, x, M, H, I, w_gu: "Tiled", w_down: "Tiled", w3: "Tiled", out3, eps, tags, epoch_ctr, epoch_add, err,
-           epoch_mul=0):
-    """qt_cp_mlp (one persistent launch): x[:M] += down(SwiGLU(gate_up(rms(x16)))); x16 = bf16(x);
-    out3[:M] = rms(x16) . w3.  tags: zeroed uint8 scratch of cp_mlp_tags_bytes(H, I); the launch's tag base is
-    epoch_ctr[0] * epoch_mul + epoch_add (distinct per launch until tags is zeroed again)."""
-    a = _hip.CpMlpArgs()
-    a.M, a.H, a.I, a.N3 = M, H, I, w3.N
-    a.x16, a.ldx16, a.x, a.ldx = ptr(x16), x16.stride(0), ptr(x), x.stride(0)
-    a.w_gu, a.w_down, a.w3, a.eps = ptr(w_gu.w), ptr(w_down.w), ptr(w3.w), eps
-    a.out3, a.ldo3 = ptr(out3), out3.stride(0)
-    a.tags, a.tags_bytes = ptr(tags), tags.numel() * tags.element_size()
-    a.epoch_ctr, a.epoch_mul, a.epoch_add, a.err = ptr(epoch_ctr), epoch_mul, epoch_add, ptr(err)
-    check(_hip.lib().qt_cp_mlp(ctypes.byref(a), stream()), "qt_cp_mlp")
-
-
 def qkv_post(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos, row_batch, kv_pos, q_out, kc, vc, Lmax):
     a = _hip.QkvArgs()
     a.R, a.Hq, a.Hkv, a.D = R, Hq, Hkv, D
@@ -282,9 +242,11 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
            codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None, algo=0,
-           ctr_stride=0, philox_row=None):
+           ctr_stride=0, philox_row=None, force=None, pick=None):
     """step / n_generated: device int32 counters, one per row when ctr_stride = 1 (0: shared); philox_row: optional
     device int32 [R] Philox stream ids (default row_base + r).
+    force / pick (teacher forcing, parity diagnostics): int32 buffers in the layout of `codes`; the choice is stored
+    in pick and the row continues with force's token.
     emb = (table fp32 [V][D], out fp32 rows, ld): also write the chosen token's table row to out[r];
     emb16 = (out bf16 rows, ld): its bf16 copy; emb2 = (table2 fp32 [V][D2], out2 fp32 rows, ld2): a second row.
     seed_ptr: device int64 [1] read at run time instead of `seed` (graph-captured samplers)."""
@@ -300,6 +262,7 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
     a.row_base = row_base
     a.seed_ptr, a.debug_u, a.algo = ptr(seed_ptr), float(debug_u), int(algo)
     a.ctr_stride, a.philox_row = int(ctr_stride), ptr(philox_row)
+    a.force, a.pick = ptr(force), ptr(pick)
     if emb is not None:
         a.emb_table, a.emb_dim, a.emb_out, a.emb_ld = ptr(emb[0]), emb[0].shape[1], ptr(emb[1]), emb[2]
         if emb16 is not None:

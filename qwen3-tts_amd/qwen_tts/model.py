@@ -10,7 +10,6 @@ from typing import Dict, List, Optional
 
 import torch
 
-from . import kernels as K
 from .talker import GenParams, TalkerEngine
 
 
@@ -227,9 +226,13 @@ class TTSModel:
                  speakers=None, non_streaming_mode=False, max_new_tokens=4096, do_sample=True, top_k=50, top_p=1.0,
                  temperature=0.9, subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0,
                  subtalker_temperature=0.9, eos_token_id=None, repetition_penalty=1.05, ignore_eos=False, seed=None,
-                 use_graph=True, max_batch=None, **kwargs):
+                 use_graph=True, max_batch=None, philox_ids=None, frame_caps=None, **kwargs):
         """Same contract as Qwen3TTSForConditionalGeneration.generate (M:2022-2292):
         returns (list of [F_i,16] int64 codes, list of [F_i,H] last hidden states).
+
+        philox_ids (not in the reference): the sampling stream id of each request (default its index in this call);
+        the data-parallel runner (qwen_tts.dp.dp_generate) passes global request indices.  frame_caps (not in the
+        reference): per-request frame limits below max_new_tokens - 1 (decoded through serve()).
 
         max_batch (not in the reference): with more requests than max_batch, decode them by continuous batching
         through max_batch batch rows (TalkerEngine.serve: a row is refilled with the next request as soon as its
@@ -240,14 +243,31 @@ class TTSModel:
         gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
                        subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
         B, P = emb.shape[0], emb.shape[1]
-        if max_batch is not None and B > int(max_batch):
+        if (max_batch is not None and B > int(max_batch)) or frame_caps is not None:
             n_real = mask.sum(-1).tolist()
-            reqs = [(emb[i, P - int(n_real[i]):], trail[i]) for i in range(B)]
+            reqs = [(emb[i, P - int(n_real[i]):], trail[i], None if frame_caps is None else frame_caps[i])
+                    for i in range(B)]
+            max_batch = B if max_batch is None else max_batch
             codes, hid = [None] * B, [None] * B
-            for i, c, h in self.engine.serve(reqs, pad, gp, slots=int(max_batch), use_graph=use_graph):
+            for i, c, h in self.engine.serve(reqs, pad, gp, slots=int(max_batch), use_graph=use_graph,
+                                             philox_ids=philox_ids):
                 codes[i], hid[i] = c, h
             return codes, hid
-        return self.engine.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=use_graph)
+        return self.engine.generate_from_embeds(emb, mask, trail, pad, gp, use_graph=use_graph, philox_ids=philox_ids)
+
+    @torch.no_grad()
+    def teacher_forced(self, ref_codes, input_ids=None, instruct_ids=None, ref_ids=None, voice_clone_prompt=None,
+                       languages=None, speakers=None, non_streaming_mode=False, repetition_penalty=1.05,
+                       eos_token_id=None, use_graph=True, **kwargs):
+        """Greedy choices of this path at every step of the reference's own code sequence (parity diagnostics; not in
+        the reference): the prompt is assembled as generate() does, each talker / code-predictor argmax is recorded
+        and then replaced by the reference token of ref_codes (list of [F_b, 16]).  Returns (picks [B, F, 16], hidden
+        [B, F, H]) so a bf16 run can be compared with fp32 reference codes position by position."""
+        emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
+                                                   voice_clone_prompt, ref_ids)
+        gp = GenParams(max_new_tokens=2, do_sample=False, subtalker_dosample=False, eos_token_id=eos_token_id,
+                       repetition_penalty=repetition_penalty)
+        return self.engine.teacher_forced(emb, mask, trail, pad, gp, ref_codes, use_graph=use_graph)
 
     # -------------------------------------------------------------------------------- streaming
     REF_CHUNK, REF_CTX = 300, 25  # Qwen3TTSTokenizerV2Decoder.chunked_decode (K:885-895)
@@ -405,7 +425,7 @@ class TTSModel:
             # prefills and generates the first frames on this one
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(main)
-            with torch.cuda.stream(side), K.use_workspace(K.new_workspace(dev)):
+            with torch.cuda.stream(side):  # (the stream's state slot brings its own split-K workspace)
                 cs = dec.stream(B, RX + RC)
                 fed = min(min(R), RC)
                 cs.feed(torch.stack([x[:fed] for x in pre]))

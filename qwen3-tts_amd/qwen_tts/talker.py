@@ -11,6 +11,7 @@ Per-request state lives in a `Session` object, never on the module (fixes the re
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -71,28 +72,28 @@ class _Stack:
         self.wdt = wdt
 
     def ensure_rope(self, npos, dev):
+        """Grow the RoPE tables to >= npos positions.  The old tables stay alive: graphs captured by other sessions
+        (frame / prefill graphs of pooled sessions) keep reading them, and they hold the same values."""
         if self.cos.shape[0] < npos:
-            self.cos, self.sin = K.rope_tables(self.D, self.theta, npos, dev)
+            self._old_rope = getattr(self, "_old_rope", []) + [(self.cos, self.sin)]
+            self.cos, self.sin = K.rope_tables(self.D, self.theta, max(npos, 2 * self.cos.shape[0]), dev)
 
-    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None, qkv0=False, mlp=None):
+    def forward(self, x, R, meta, kv, scratch, Lmax, max_keys, decode=False, x16=None, qkv0=False):
         """x fp32 [R][H] residual stream, updated in place.  meta: dict of int32 device row arrays.
         decode=True: one row per batch entry attending to its own prefix -> fused qt_decode_attention.
         x16 (bf16 mode, R <= 16): bf16 shadow of x, kept current by every writer of x (the residual-add epilogues
         store both) and read as the A operand of the RMS-normalised GEMVs (QKV, gate/up): their MFMA rounds A to
         bf16 anyway, so only the RMS row sums change (they come from the bf16 values, as the reference's bf16
         residual stream gives them) while the activation fetch halves.
-        qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler).
-        mlp (code-predictor decode, bf16 + x16): {"tags", "ctr", "err", "base", "head": (W, out)} -- each layer's MLP
-        and the next RMS GEMV (next layer's q/k/v, or the head W into out) as one persistent qt_cp_mlp launch."""
+        qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler)."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
-        if x16 is not None and ("mlp_ws" in scratch or (R > 96 and not PF)):
-            x16 = None  # the fused MLP / igemm_k write x only (decode / skinny GEMVs and gemm_pf_k keep the shadow)
+        if x16 is not None and R > 96 and not PF:
+            x16 = None  # igemm_k writes x only (decode / skinny GEMVs and gemm_pf_k keep the shadow)
         xa = x if x16 is None else x16
-        use_mlp = mlp is not None and fused_ao and x16 is not None and R <= 16
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            if not (qkv0 and li == 0) and not (use_mlp and li > 0):
+            if not (qkv0 and li == 0):
                 K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
@@ -111,21 +112,10 @@ class _Stack:
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             if not fused_ao:
                 K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD, out2=x16)
-            if use_mlp:  # gate/up -> down -> the next RMS GEMV in one persistent launch
-                w3, o3 = (self.layers[li + 1].qkv, scratch["qkv"]) if li + 1 < len(self.layers) else mlp["head"]
-                K.cp_mlp(x16, x, R, self.H, self.I, L.gu, L.down, w3, o3, self.eps, mlp["tags"], mlp["ctr"],
-                         mlp["base"] + li, mlp["err"])
-            elif "mlp_ws" in scratch and R <= 16:  # one fused launch: RMSNorm + gate/up + SwiGLU + down + residual
-                K.mlp_decode(x, R, self.H, self.I, L.gu, L.down, self.eps, scratch["mlp_ws"], scratch["mlp_err"])
-            else:
-                K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
-                K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD, out2=x16)
+            K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD, out2=x16)
 
 
-# qt_mlp_decode (one-launch MLP) is correct and tested but measured slower than the two GEMVs on MI355X
-# (CP 17.1 vs 14.6 us, talker 31.6 vs 22.8 us: its 96-192 blocks stream the weights through fewer CUs and the
-# cross-block reduction adds ~3 dependent round trips), so it is opt-in.
-FUSED_MLP = os.environ.get("QT_FUSED_MLP", "0") == "1"
 # code-predictor decode steps: qt_decode_attn_oproj (attention fused into o_proj + residual); QT_ATTN_OPROJ=0 keeps
 # the two-launch path (decode attention, then the o_proj GEMV) for A/B measurement
 ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
@@ -133,17 +123,29 @@ ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
 QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
-# code-predictor decode MLP + next RMS GEMV as one persistent launch (qt_cp_mlp, bf16 mode; QT_CP_MLP=1): correct
-# and tested, but measured slower than the three GEMV launches it replaces (16.5 vs 13.9 us per layer, CP step 122
-# vs 110 us; profiles/r02_cp_mlp_persistent_ab.txt): each in-launch tagged hand-off costs as much as the kernel
-# boundary it removes, so it is opt-in
-CP_MLP = os.environ.get("QT_CP_MLP", "0") == "1"
 # talker prefill captured into a HIP graph per (session, prompt length) once that length repeats; QT_PREFILL_GRAPH=0
 # always issues it eagerly (A/B)
 PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
 # large-M prefill linears on gemm_pf_k (LDS-staged bf16 A and B): the prefill keeps the bf16 residual shadow at any
 # row count, so its RMS GEMMs read bf16 A too; QT_PF=0 (read by the library as well) keeps igemm_k (A/B)
-PF = os.environ.get("QT_PF", "1") != "0"
+PF = _hip.env_int("QT_PF", 1) != 0  # parsed as the library parses it (C atoi)
+# static prefill buffers (+ captured graphs) kept per session: the most recently used prompt lengths, LRU-evicted
+PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
+
+
+def _lru_get(d: OrderedDict, key):
+    v = d.get(key)
+    if v is not None:
+        d.move_to_end(key)
+    return v
+
+
+def _lru_put(d: OrderedDict, key, v):
+    """Insert, evicting the least recently used prompt lengths beyond PREFILL_CACHE (their buffers and any graph
+    captured over them go together: nothing else references them)."""
+    d[key] = v
+    while len(d) > PREFILL_CACHE:
+        d.popitem(last=False)
 
 
 def _scratch(R, st: _Stack, dev, attn_oproj=False):
@@ -154,9 +156,6 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
     sc = {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
     sc["attn_oproj"] = attn_oproj and ATTN_OPROJ and _attn_oproj_ok(st)
-    if FUSED_MLP and R <= 16 and K.mlp_supported(st.H, st.I, st.wdt):  # fused decode MLP scratch
-        sc["mlp_ws"] = torch.zeros(K.mlp_ws_bytes(R, st.H, st.I), dtype=torch.uint8, device=dev)
-        sc["mlp_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
     return sc
 
 
@@ -191,12 +190,6 @@ class CPLane:
         p2 = torch.arange(2 * nb, device=dev, dtype=torch.int32) % 2
         self.meta0 = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(2 * nb),
                       "row_batch": rb2, "small_T": 2}
-        # persistent code-predictor MLP (qt_cp_mlp, bf16 mode): hand-off tag buffer (zeroed once per frame), a zero
-        # epoch word (the tag base is a per-launch constant of the frame graph) and the time-out flag
-        self.mlp = None
-        if self.x16 is not None and eng.cp_mlp_ok(nb):
-            self.mlp = {"tags": torch.zeros(K.cp_mlp_tags_bytes(c.H, c.I), dtype=torch.uint8, device=dev),
-                        "ctr": i32(1), "err": i32(1)}
         rb = torch.arange(nb, dtype=torch.int32, device=dev)
         self.meta = []
         for g in range(1, s.G - 1):
@@ -239,7 +232,7 @@ class GenParams:
 class Session:
     """Device buffers + captured frame graph for one (batch, capacity, params) shape."""
 
-    def __init__(self, eng: "TalkerEngine", B: int, P_cap: int, max_frames: int, gp: GenParams):
+    def __init__(self, eng: "TalkerEngine", B: int, P_cap: int, max_frames: int, gp: GenParams, teacher=False):
         dev, t, c = eng.dev, eng.talker, eng.cp
         self.B, self.P_cap, self.max_frames, self.gp = B, P_cap, max_frames, gp
         self.Lmax = P_cap + max_frames + 2
@@ -263,7 +256,7 @@ class Session:
         f32 = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.x = f32(B, t.H)
         # bf16 shadows of the decode residual streams (bf16 mode): A operands of the RMS-normalised GEMVs
-        use16 = eng.wdt == torch.bfloat16 and not FUSED_MLP and X16  # the fused MLP writes x only
+        use16 = eng.wdt == torch.bfloat16 and X16
         bf = lambda *s: torch.zeros(*s, dtype=torch.bfloat16, device=dev) if use16 else None  # noqa: E731
         self.x16 = bf(B, t.H)
         self.cp_x16 = bf(2 * B, c.H)
@@ -272,6 +265,9 @@ class Session:
         self.cp_x = f32(2 * B, c.H)
         self.sc_t = _scratch(B, t, dev)
         self.codes = i32(B, max_frames + 2, self.G)
+        # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
+        self.force = i32(B, max_frames + 2, self.G) if teacher else None
+        self.pick = i32(B, max_frames + 2, self.G) if teacher else None
         self.hiddens = f32(B, max_frames + 2, t.H)  # + the frame a capped row re-runs (serve())
         self.tok0 = i32(B)
         self.cp_tok = i32(B)
@@ -283,8 +279,9 @@ class Session:
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox key, read by the captured samplers
         self.row_base = 0
         self.graph = None
-        self.prefill = {}  # prompt length P -> static prefill buffers (+ captured graph once P repeats)
-        self.slot_prefill = {}  # prompt length P -> static single-request prefill buffers (serve() refills)
+        # prompt length P -> static prefill buffers (+ captured graph once P repeats); LRU, PREFILL_CACHE lengths
+        self.prefill = OrderedDict()
+        self.slot_prefill = OrderedDict()  # P -> static single-request prefill buffers (serve() refills); LRU
         self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
         nl = max(1, min(eng.cp_lanes, B))
         cuts = [B * i // nl for i in range(nl + 1)]
@@ -304,7 +301,8 @@ class TalkerEngine:
         self.G = tc["num_code_groups"]
         self.V, self.Vc = tc["vocab_size"], cc["vocab_size"]
         W, dev, wdt = weights, self.dev, self.wdt
-        self.talker = _Stack(W, "talker.model", tc, wdt, dev, 4096)
+        # RoPE positions for prompt + max_new_tokens (4096) without regrowing in the common case
+        self.talker = _Stack(W, "talker.model", tc, wdt, dev, 8192)
         self.cp = _Stack(W, "talker.code_predictor.model", cc, wdt, dev, self.G + 2)
         self.codec_head = K.tile_linear(_w(W, "talker.codec_head.weight", dev), wdt)
         self.emb0 = _w(W, "talker.model.codec_embedding.weight", dev).to(wdt).contiguous()
@@ -346,14 +344,6 @@ class TalkerEngine:
         self._cp_streams: List[torch.cuda.Stream] = []
         torch.cuda.synchronize()
 
-    def cp_mlp_ok(self, rows: int) -> bool:
-        """qt_cp_mlp serves this code predictor's decode steps at `rows` rows (bf16 weights, fused attention + o_proj,
-        supported dims, >= 256 CUs); QT_CP_MLP=0 keeps the launch-per-GEMV form (A/B measurement)."""
-        c = self.cp
-        return (CP_MLP and self.wdt == torch.bfloat16 and _attn_oproj_ok(c) and ATTN_OPROJ
-                and K.cp_mlp_supported(rows, c.H, c.I, c.qkv_w) and K.cp_mlp_supported(rows, c.H, c.I, self.Vc)
-                and all(L.gu.dtype == torch.bfloat16 for L in c.layers))
-
     def _proj_table(self, emb, Hc):
         """small_to_mtp(embedding table) (M:1299 applied row-wise) or the table itself, fp32 [V][Hc]."""
         V = emb.shape[0]
@@ -391,12 +381,12 @@ class TalkerEngine:
         return out
 
     # ---------------------------------------------------------------- sessions / graph
-    def session(self, B, P, max_frames, gp: GenParams, row_base: int = 0) -> Session:
+    def session(self, B, P, max_frames, gp: GenParams, row_base: int = 0, teacher: bool = False) -> Session:
         """A free session of this shape, marked busy (release() hands it back).  A session held by a live request
         (e.g. a suspended stream() generator) is never shared: a concurrent request of the same shape gets a
         session of its own (own KV cache, counters and captured graph)."""
         P_cap = max(64, (P + 63) // 64 * 64)
-        key = (B, max_frames, gp.key(), row_base)
+        key = (B, max_frames, gp.key(), row_base, teacher)
         pool = self._sessions.setdefault(key, [])
         for s in pool:
             if not s.busy and s.P_cap >= P:
@@ -412,7 +402,7 @@ class TalkerEngine:
                 self._sessions[k] = [s for s in self._sessions[k] if s.busy]
         for k in [k for k, v in self._sessions.items() if not v and k != key]:
             del self._sessions[k]
-        s = Session(self, B, P_cap, max_frames, gp)
+        s = Session(self, B, P_cap, max_frames, gp, teacher=teacher)
         s.row_base = row_base
         self.talker.ensure_rope(s.Lmax + 4, self.dev)
         self._sessions.setdefault(key, []).append(s)
@@ -449,7 +439,8 @@ class TalkerEngine:
                  codes=s.codes[b0:b1], codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=0,
                  codes_step_off=codes_step_off, ctr_stride=1, philox_row=s.prow[b0:b1],
                  emb=(self.cp_in_tab0, s.cp_x.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc),
-                 emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc))
+                 emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc),
+                 force=None if s.force is None else s.force[b0:b1], pick=None if s.pick is None else s.pick[b0:b1])
 
     def _frame(self, s: Session):
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
@@ -496,22 +487,16 @@ class TalkerEngine:
         p16 = ln.x16 if 2 * nb <= 96 else None  # forward() keeps the shadow for decode / skinny-GEMV row counts
         c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
         self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
-        if ln.mlp is not None:
-            ln.mlp["tags"].zero_()  # tag bases below are per-launch constants, distinct within one frame
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
             x16 = None if ln.x16 is None else ln.x16[:nb]
-            mlp = None
-            if ln.mlp is not None:
-                mlp = dict(ln.mlp, base=1 + (g - 1) * len(c.layers), head=(self.lm_heads[g], ln.logits))
             c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16,
-                      qkv0=self.cp_qkv_tabs is not None, mlp=mlp)
-            self._cp_head(s, ln, x, Hc, g, x16, logits_ready=mlp is not None)
+                      qkv0=self.cp_qkv_tabs is not None)
+            self._cp_head(s, ln, x, Hc, g, x16)
 
-    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None, logits_ready=False):
+    def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None):
         c, gp = self.cp, s.gp
-        if not logits_ready:  # (else the last layer's qt_cp_mlp launch computed them)
-            K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
+        K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed_ptr=s.seed, step=s.step[ln.b0:ln.b1], substep=1 + g, codes=ln.codes,
@@ -520,27 +505,62 @@ class TalkerEngine:
                  emb=(self.cp_in_tabs[g], ln.x, c.H) if g < self.G - 2 else None,
                  emb16=(ln.x16, c.H) if ln.x16 is not None and g < self.G - 2 else None,
                  emb2=(self.cp_qkv_tabs[g], ln.sc["qkv"], c.qkv_w) if self.cp_qkv_tabs is not None and g < self.G - 2
-                 else None)
+                 else None,
+                 force=None if s.force is None else s.force[ln.b0:ln.b1],
+                 pick=None if s.pick is None else s.pick[ln.b0:ln.b1])
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
                              tts_pad: torch.Tensor, gp: GenParams, use_graph: bool = True, on_frames=None,
-                             groups: Optional[int] = None):
+                             groups: Optional[int] = None, philox_ids=None):
         """embeds fp32 [B,P,H] left-padded, mask [B,P] -> (codes list [F_i,16] int64 cpu, hidden list).
 
         The batch is decoded as `groups` independent row groups (default self.row_groups), each on its own
         HIP stream with its own session and captured frame graph; per-row arithmetic (and, through row_base,
-        each row's Philox stream) is the same as decoding the batch whole."""
+        each row's Philox stream) is the same as decoding the batch whole.  philox_ids: optional per-row Philox
+        stream ids (default the row index) -- a data-parallel shard passes its requests' global indices, so every
+        request draws the same stream whichever rank and row decode it."""
         it = self.decode_iter(embeds, mask, trailing, tts_pad, gp, use_graph=use_graph, on_frames=on_frames,
-                              groups=groups)
+                              groups=groups, philox_ids=philox_ids)
         out = None
         for sessions, frames, final in it:
             if final:  # collected while the sessions are still held by this request
                 out = self.collect(sessions, frames)
         return out
 
+    def teacher_forced(self, embeds, mask, trailing, tts_pad, gp: GenParams, ref_codes, use_graph: bool = True):
+        """Teacher-forced decode (parity diagnostics): every token choice -- the talker's cb0 and the code
+        predictor's 15 -- is made by this path's processors and argmax as in generate(), recorded, and then replaced by
+        the reference's token, so each step sees exactly the reference's history.  ref_codes: per row [F_b, 16].
+        Returns (picks [B, F, 16] int64 cpu in the codes' layout, hidden [B, F, H] cpu), F = max F_b; entries past a
+        row's F_b are unspecified."""
+        import dataclasses
+        B, P, H = embeds.shape
+        F = max(int(c.shape[0]) for c in ref_codes)
+        gp = dataclasses.replace(gp, max_new_tokens=F + 1)
+        s = self.session(B, P, max(F, 1), gp, teacher=True)
+        try:
+            s.force.zero_()
+            for b, c in enumerate(ref_codes):
+                s.force[b, :c.shape[0]] = torch.as_tensor(c).to(self.dev, torch.int32)
+            with K.use_workspace(s.ws):
+                self._prefill(s, embeds, mask, trailing, tts_pad, gp.resolve_seed())
+                if use_graph and s.graph is None:
+                    s.graph = self._capture(s)
+            s.hiddens[:, 0].copy_(s.past_hidden)
+            for _ in range(F):
+                if use_graph:
+                    s.graph.replay()
+                else:
+                    with K.use_workspace(s.ws):
+                        self._frame(s)
+            return s.pick[:, :F].long().cpu(), s.hiddens[:, :F].cpu()
+        finally:
+            self.release([s])
+
     def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
-                    groups: Optional[int] = None, every: int = 0, first: int = 0, grow: bool = False):
+                    groups: Optional[int] = None, every: int = 0, first: int = 0, grow: bool = False,
+                    philox_ids=None):
         """Prefill + frame loop as a generator: yields (sessions, frames_done, final) after `first` frames, then
         every `every` frames (0: only at the end; grow=True: intervals double from first - 1 up to `every`), and once
         at the end with final=True.  codes[:, :frames_done]
@@ -561,7 +581,8 @@ class TalkerEngine:
                 s = self.session(b1 - b0, P, max(max_frames, 1), gp, row_base=b0)
                 sessions.append(s)
                 with torch.cuda.stream(st), K.use_workspace(s.ws):
-                    self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad, seed)
+                    self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad, seed,
+                                  None if philox_ids is None else philox_ids[b0:b1])
                     if max_frames > 0 and use_graph and s.graph is None:
                         s.graph = self._capture(s)
                 streams.append(st)
@@ -616,14 +637,6 @@ class TalkerEngine:
                     break
         for st in streams:
             main.wait_stream(st)
-        for s in sessions:
-            for sc in [s.sc_t] + [ln.sc for ln in s.cp_lanes]:
-                if "mlp_err" in sc and int(sc["mlp_err"].item()):
-                    raise RuntimeError("qt_mlp_decode: in-kernel arrival wait timed out (results invalid)")
-            for ln in s.cp_lanes:
-                if ln.mlp is not None and int(ln.mlp["err"].item()):
-                    ln.mlp["err"].zero_()
-                    raise RuntimeError("qt_cp_mlp: an in-launch hand-off wait timed out (results invalid)")
         yield sessions, frames, True
 
     def collect(self, sessions, frames):
@@ -642,7 +655,8 @@ class TalkerEngine:
         return out_c, out_h
 
     # ---------------------------------------------------------------- continuous batching
-    def serve(self, requests, tts_pad, gp: GenParams, slots: int = 8, use_graph: bool = True, poll: int = 4):
+    def serve(self, requests, tts_pad, gp: GenParams, slots: int = 8, use_graph: bool = True, poll: int = 4,
+              philox_ids=None):
         """Continuous batching: decode `requests` through `slots` batch rows of one session, refilling a row with
         the next queued request as soon as its request ends (EOS, or max_new_tokens - 1 frames) instead of padding
         it with EOS until the whole batch ends as the reference's batched generate() does (M:2272-2292).
@@ -652,12 +666,17 @@ class TalkerEngine:
         max_new_tokens - 1 frames (it is retired at the first poll past it, so its row may run up to `poll` frames
         longer).  Yields (i, codes [F_i, 16] int64 cpu, hidden [F_i, H] cpu)
         as requests finish (completion order).  Request i draws Philox stream i of the call's seed, i.e. the
-        stream row i of a one-shot batched generate() of the same list draws, whichever slot decodes it.
+        stream row i of a one-shot batched generate() of the same list draws, whichever slot decodes it.  Per request
+        the result equals the one-shot batch's up to GEMM summation order: a refill prefills P rows while the batch
+        prefills B x P, and at production sizes the two row counts can take different GEMM kernels (skinny GEMV /
+        split-K vs gemm_pf_k), so in bf16 a near-tie may resolve differently (fp32: identical in the tests).
 
         The frame graph is the session's ordinary captured frame (per-row step / position counters); a refill is
         a single-request prefill into the slot's K/V rows between two graph replays.  The host learns which rows
-        ended from pinned copies of the device flags every `poll` frames (no host sync on the decode stream)."""
+        ended from pinned copies of the device flags every `poll` frames (no host sync on the decode stream).
+        philox_ids: optional Philox stream id per request (default its index i)."""
         n = len(requests)
+        pids = list(range(n)) if philox_ids is None else [int(x) for x in philox_ids]
         if n == 0:
             return
         B = max(1, min(slots, n))
@@ -682,7 +701,7 @@ class TalkerEngine:
                     emb[b, Pb - e.shape[0]:] = e
                     mask[b, Pb - e.shape[0]:] = 1
                     trail[b, :tr.shape[0]] = tr
-                self._prefill(s, emb, mask, trail, tts_pad, seed)
+                self._prefill(s, emb, mask, trail, tts_pad, seed, pids[:B])
                 s.hiddens[:, 0].copy_(s.past_hidden)
                 queue = list(range(B, n))
                 slot_req = list(range(B))
@@ -733,7 +752,7 @@ class TalkerEngine:
                         start[b] = frame
                         slot_req[b] = queue.pop(0) if queue else -1
                         if slot_req[b] >= 0:
-                            self._prefill_slot(s, b, requests[slot_req[b]], slot_req[b])
+                            self._prefill_slot(s, b, requests[slot_req[b]], pids[slot_req[b]])
                         else:
                             s.finished[b:b + 1].fill_(1)  # idle slot: emits EOS until the session ends
                     while harvests and harvests[0][-1].query():
@@ -749,8 +768,8 @@ class TalkerEngine:
             self.release([s])
 
     def _prefill_slot(self, s: Session, b: int, req, i: int):
-        """Start request i in batch row b: per-row state reset, single-request talker prefill into row b's K/V
-        (positions 0..P-1, no left padding), first token (M:1746-1800, 2044)."""
+        """Start a request in batch row b (Philox stream id i): per-row state reset, single-request talker prefill into
+        row b's K/V (positions 0..P-1, no left padding), first token (M:1746-1800, 2044)."""
         emb, trail = req[0], req[1]
         P, H = int(emb.shape[0]), self.talker.H
         t, dev = self.talker, self.dev
@@ -769,7 +788,7 @@ class TalkerEngine:
         tr.copy_(s.pad_embed.view(1, H).expand_as(tr))
         nt = min(int(trail.shape[0]), tr.shape[0])
         tr[:nt] = trail[:nt].to(dev).float()
-        pre = s.slot_prefill.get(P)
+        pre = _lru_get(s.slot_prefill, P)
         if pre is None:
             i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
             ar = torch.arange(P, device=dev, dtype=torch.int32)
@@ -778,7 +797,7 @@ class TalkerEngine:
                             "row_batch": i32(P)},
                    "x16": (torch.empty(P, H, dtype=torch.bfloat16, device=dev)
                            if X16 and self.wdt == torch.bfloat16 and (P <= 96 or PF) else None)}
-            s.slot_prefill[P] = pre
+            _lru_put(s.slot_prefill, P, pre)
         pre["meta"]["row_batch"].fill_(b)
         pre["x"].copy_(emb.reshape(P, H))
         if pre["x16"] is not None:
@@ -789,8 +808,9 @@ class TalkerEngine:
         K.gemm(s.past_hidden[b:b + 1], self.codec_head, s.logits[b:b + 1], 1, H, self.V)
         self._sample_talker(s, s.logits, 0, 99, b, b + 1)
 
-    def _prefill(self, s: Session, embeds, mask, trailing, tts_pad, seed: int):
-        """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s."""
+    def _prefill(self, s: Session, embeds, mask, trailing, tts_pad, seed: int, philox_ids=None):
+        """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s.
+        philox_ids: per-row Philox stream ids (default row_base + row)."""
         B, P, H = embeds.shape
         t = self.talker
         dev = self.dev
@@ -798,7 +818,10 @@ class TalkerEngine:
         for z in (s.seen, s.finished, s.codes, s.ctr):
             z.zero_()
         s.seed.fill_(seed)
-        torch.arange(s.row_base, s.row_base + B, dtype=torch.int32, device=dev, out=s.prow)
+        if philox_ids is None:
+            torch.arange(s.row_base, s.row_base + B, dtype=torch.int32, device=dev, out=s.prow)
+        else:
+            s.prow.copy_(_to_dev_i32(list(philox_ids), dev))
         # stale K/V beyond each row's valid range is never read (row_start/row_len bound every read)
         Ttr = trailing.shape[1]
         s.pad_embed.copy_(tts_pad.reshape(-1).float())
@@ -814,7 +837,7 @@ class TalkerEngine:
         n_pads = P - n_real
         rope_delta = (max_pos + 1 - n_real).long() - n_pads
         R = B * P
-        pre = s.prefill.get(P)
+        pre = _lru_get(s.prefill, P)
         if pre is None:  # static buffers of this prompt length (a captured graph binds their addresses)
             i32 = lambda *z: torch.zeros(*z, dtype=torch.int32, device=dev)  # noqa: E731
             pre = {"x": torch.empty(R, H, dtype=torch.float32, device=dev), "sc": _scratch(R, t, dev),
@@ -826,7 +849,7 @@ class TalkerEngine:
                    # bf16 shadow of the prefill residual (skinny-GEMV row counts): the RMS GEMVs read half the bytes
                    "x16": (torch.empty(R, H, dtype=torch.bfloat16, device=dev)
                            if X16 and self.wdt == torch.bfloat16 and (R <= 96 or PF) else None)}
-            s.prefill[P] = pre
+            _lru_put(s.prefill, P, pre)
         pre["meta"]["rope_pos"].copy_(pos.reshape(-1))
         pre["meta"]["row_start"].copy_(torch.where(mask.bool(), n_pads[:, None], torch.zeros_like(n_pads)[:, None])
                                        .reshape(-1))

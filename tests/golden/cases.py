@@ -47,6 +47,47 @@ def talker_cases():
     }
 
 
+FULL_SPEAKERS = ["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"]
+
+
+def full_cases():
+    """Production-shape greedy cases (BASELINE.json configs[1] / configs[2]): reference codes, per-pick
+    top-2 margins and first hidden states are in tests/golden/full_<key>.npz.  `idx` seeds the token ids."""
+    return {
+        # configs[2]: 1.7B CustomVoice, B=8 x 200-token prompts, streaming text (trailing text fed per frame)
+        "cv17_b8_stream": dict(preset="1.7b-customvoice", idx=60, texts=[200] * 8, languages=["english"] * 8,
+                               speakers=FULL_SPEAKERS, non_streaming_mode=False, max_new_tokens=33),
+        # configs[1]: 0.6B CustomVoice, 1 utterance of 120 text tokens, non-streaming (Identity small_to_mtp, M:1174)
+        "cv06_b1_nonstream": dict(preset="0.6b-customvoice", idx=61, texts=[120], languages=["english"],
+                                  speakers=["vivian"], non_streaming_mode=True, max_new_tokens=49),
+    }
+
+
+def margins_grid(flat, B, n_tokens, groups=16):
+    """oracle.generate(record_margins=True) logs the top-2 margin of every greedy pick in generation order: per talker
+    step the B cb0 picks, then (if the loop continues) the code predictor's 15 x B picks.  Returns [B, frames, 16] in
+    the layout of the codes (frame f = cb0 of step f + the CP codes drawn during step f+1)."""
+    a = np.asarray(flat, dtype=np.float32)
+    frames = n_tokens - 1
+    a = a[:frames * groups * B].reshape(frames, groups, B)
+    return np.ascontiguousarray(a.transpose(2, 0, 1))
+
+
+def first_divergence(got, ref, margins, tol):
+    """Per row: first (frame, group) in generation order where `got` differs from `ref`.  Returns a list of
+    (row, flat index or None, reference margin there)."""
+    out = []
+    for b, (g, r) in enumerate(zip(got, ref)):
+        n = min(g.shape[0], r.shape[0])
+        d = np.flatnonzero((np.asarray(g[:n]) != np.asarray(r[:n])).reshape(-1))
+        if d.size == 0:
+            out.append((b, None, None))
+        else:
+            i = int(d[0])
+            out.append((b, i, float(margins[b].reshape(-1)[i])))
+    return out
+
+
 def make_inputs(case, idx, H):
     ids = [text_ids(n, 100 * idx + j) for j, n in enumerate(case["texts"])]
     ins = None

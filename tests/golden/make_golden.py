@@ -148,7 +148,7 @@ def make_tiny_talker(preset="tiny-customvoice"):
     np.savez_compressed(os.path.join(HERE, "tiny_talker.npz"), **out)
 
 
-def make_codec(preset, cases, fname):
+def make_codec(preset, cases, fname, stride=7):
     dec, ccfg = build_ref_codec(preset)
     out = {}
     g = np.random.default_rng(4321)
@@ -161,7 +161,8 @@ def make_codec(preset, cases, fname):
             out[f"{key}/codes{j}"] = c.astype(np.int32)
             out[f"{key}/len{j}"] = np.array(w.shape[0])
             if w.shape[0] > 200_000:  # keep fixtures small: strided samples + checksums for long outputs
-                out[f"{key}/wav{j}_stride"] = w[::7].copy()
+                out[f"{key}/stride"] = np.array(stride)
+                out[f"{key}/wav{j}_stride"] = w[::stride].copy()
                 out[f"{key}/wav{j}_sum"] = np.array([w.astype(np.float64).sum(), (w.astype(np.float64) ** 2).sum()])
             else:
                 out[f"{key}/wav{j}"] = w
@@ -247,25 +248,43 @@ def make_specs():
         json.dump(specs, f)
 
 
-def make_full(preset="1.7b-customvoice", frames=32):
-    t0 = time.time()
-    model, cfg = build_ref_model(preset)
-    print(f"  built {preset} in {time.time() - t0:.0f}s")
-    H = cfg["talker_config"]["hidden_size"]
-    out = {}
-    for key, case in {"full_b1": dict(texts=[120], languages=["english"], speakers=["vivian"],
-                                      non_streaming_mode=True, max_new_tokens=frames + 1),
-                      "full_b4_stream": dict(texts=[40, 25, 33, 18], languages=["english"] * 4,
-                                             speakers=["vivian", "ryan", "serena", "aiden"],
-                                             non_streaming_mode=False, max_new_tokens=frames + 1)}.items():
+def make_full(only=None):
+    """Production-shape fixtures (cases.full_cases): the reference's greedy generate() codes at the
+    full ASSUMED dims, plus -- from the oracle, after asserting that its codes equal the reference's bit for bit --
+    the top-2 margin of the processed scores at every greedy pick ([B, frames, 16], the codes' layout) and the
+    hidden states of the first two and the last frame."""
+    from cases import full_cases, margins_grid
+    from oracle import TalkerOracle, build_prompts, generate, talker_param_specs
+    from oracle.weights import synth_state_dict
+    for key, case in full_cases().items():
+        if only and key != only:
+            continue
         t0 = time.time()
-        codes, hid = run_ref_generate(model, case, 50 + len(out), H)
-        out[f"{key}/n"] = np.array(len(codes))
-        for j, c in enumerate(codes):
-            out[f"{key}/codes{j}"] = c.numpy().astype(np.int32)
-            out[f"{key}/hidden{j}_first"] = hid[j][:2].numpy().astype(np.float32)
-        print(f"  {key}: frames {[c.shape[0] for c in codes]} ({time.time() - t0:.0f}s)")
-    np.savez_compressed(os.path.join(HERE, f"full_{preset}.npz"), **out)
+        model, cfg = build_ref_model(case["preset"])
+        H = cfg["talker_config"]["hidden_size"]
+        print(f"  {key}: built {case['preset']} in {time.time() - t0:.0f}s")
+        t0 = time.time()
+        codes, hid = run_ref_generate(model, case, case["idx"], H)
+        print(f"  {key}: reference frames {[c.shape[0] for c in codes]} ({time.time() - t0:.0f}s)")
+        del model
+        t0 = time.time()
+        o = TalkerOracle(cfg, synth_state_dict(talker_param_specs(cfg)))
+        ids, ins, vcp, ref_ids = make_inputs(case, case["idx"], H)
+        emb, mask, trail, pad = build_prompts(o, ids, case["languages"], case["speakers"], ins,
+                                              case["non_streaming_mode"], vcp, ref_ids)
+        res = generate(o, emb, mask, trail, pad, record_margins=True, **gen_kwargs(case))
+        for a, b in zip(res.codes, codes):
+            assert torch.equal(a, b), f"{key}: oracle codes differ from the reference at full dims"
+        B = len(codes)
+        mg = margins_grid(res.margins, B, res.raw_tokens.shape[1])
+        print(f"  {key}: oracle == reference ({time.time() - t0:.0f}s); min margin {mg.min():.3g}, "
+              f"#picks < 1e-3: {(mg < 1e-3).sum()} of {mg.size}")
+        out = {"n": np.array(B), "margins": mg, "prompt_len": np.array(emb.shape[1])}
+        for j, (c, h) in enumerate(zip(codes, hid)):
+            out[f"codes{j}"] = c.numpy().astype(np.int32)
+            out[f"hidden{j}_first"] = h[:2].numpy().astype(np.float32)
+            out[f"hidden{j}_last"] = h[-1:].numpy().astype(np.float32)
+        np.savez_compressed(os.path.join(HERE, f"full_{key}.npz"), **out)
 
 
 def main():
@@ -285,8 +304,13 @@ def main():
     if a.only in (None, "frontend"):
         make_frontend("tiny-base", "tiny", "frontend_tiny.npz")
         make_frontend("1.7b-base", "full", "frontend_full.npz")
-    if a.full or a.only == "full":
-        make_full()
+    if a.only in (None, "codec_chunks"):
+        # full-dim chunk restarts (K:885-895): 300 frames = one chunk, 325 / 700 = restarts with 25 frames of left
+        # context, and a ragged pair whose long row restarts while the short one is zero padding
+        make_codec("1.7b-customvoice", {"t300": [300], "t325": [325], "t700": [700], "ragged_325_40": [325, 40]},
+                   "codec_full_chunks.npz", stride=17)
+    if a.full or (a.only or "").startswith("full"):
+        make_full(a.only.split(":", 1)[1] if a.only and ":" in a.only else None)
 
 
 if __name__ == "__main__":

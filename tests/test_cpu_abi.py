@@ -9,10 +9,12 @@ def test_library_exports_every_declared_symbol():
     from qwen_tts import _hip
     L = _hip.load_library()
     hdr = open(os.path.join(REPO, "include", "qwen3tts_amd.h")).read()
-    declared = set(re.findall(r"\b(?:int|long long) (qt_\w+)\(", hdr))
+    declared = set(re.findall(r"\b(?:int|long long|const char\*) (qt_\w+)\(", hdr))
     assert declared == set(_hip.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
+    # the library is the build of the sources in this tree (content digest, not mtime)
+    assert _hip.BUILD_ID == _hip.source_digest()
 
 
 def test_qwen2_bpe_files_are_used(tmp_path):

@@ -57,3 +57,61 @@ def test_world2_gloo_broadcast_gather_timing():
     assert ok_w
     assert [r.split("@")[0] for r in res] == [f"utt{i}" for i in range(5)]
     assert dt == 2.0 and audio == 20.0
+
+
+class _StubModel:
+    """Stands in for TTSModel on CPU: 'codes' encode the request's global id, so the gather order is checkable."""
+
+    def __init__(self):
+        self.calls = []
+
+    def generate(self, input_ids, languages, speakers, instruct_ids, max_batch, philox_ids, frame_caps=None, **gen):
+        self.calls.append(dict(n=len(input_ids), max_batch=max_batch, philox_ids=list(philox_ids), caps=frame_caps))
+        codes = [torch.full((int(frame_caps[j]) if frame_caps else 3, 16), int(philox_ids[j])) for j in range(len(input_ids))]
+        return codes, None
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qwen_tts.dp import dp_generate
+    ids = [torch.zeros(1, n) for n in (5, 9, 3, 7, 11, 4, 6)]
+    frames = [10, 40, 5, 30, 20, 8, 12]
+    m = _StubModel()
+    out = dp_generate(m, ids, ["english"] * 7, None, None, frames=frames, slots=2, max_new_tokens=64)
+    # coalesced broadcast: mixed dtypes, a bucket limit that splits the fp32 tensors
+    g = torch.Generator().manual_seed(3)
+    ref = {"a": torch.randn(100, generator=g), "b": torch.randn(7, 3, generator=g), "c": torch.randn(50, generator=g),
+           "d": torch.arange(6, dtype=torch.int64), "e": torch.randn(4, generator=g).to(torch.bfloat16)}
+    W = {k: (v.clone() if rank == 0 else torch.zeros_like(v)) for k, v in ref.items()}
+    calls = broadcast_weights(W, bucket_bytes=500)
+    ok = all(torch.equal(W[k], ref[k]) for k in ref)
+    q.put((rank, out, m.calls, ok, calls))
+    dist.destroy_process_group()
+
+
+def test_world2_dp_generate_shards_and_gathers():
+    """dp_generate over 2 gloo ranks: each rank decodes its longest-first share with global Philox ids and frame caps,
+    rank 0 gets every request back in order; the weight broadcast is coalesced per dtype into bounded buckets."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=120), q.get(timeout=120)))
+    for p in ps:
+        p.join(timeout=60)
+    out, calls0, ok, ncalls = got[0]
+    assert got[1][0] is None and ok and got[1][2]
+    codes, wavs = out
+    frames = [10, 40, 5, 30, 20, 8, 12]
+    assert wavs is None and len(codes) == 7
+    for i, c in enumerate(codes):
+        assert c.shape[0] == frames[i] and int(c[0, 0]) == i
+    ids_all = sorted(calls0[0]["philox_ids"] + got[1][1][0]["philox_ids"])
+    assert ids_all == list(range(7))
+    loads = [sum(100 * frames[i] for i in c[0]["philox_ids"]) for c in (calls0, got[1][1])]
+    assert abs(loads[0] - loads[1]) <= 100 * max(frames)
+    assert ncalls == 4  # fp32 a+b (<= 500 B), fp32 c, int64 d, bf16 e

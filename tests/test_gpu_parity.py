@@ -148,37 +148,6 @@ def test_gemm_transposed_conv(cin, cout, s):
         torch.testing.assert_close(out.view(B, tout * s, cout).permute(0, 2, 1).cpu(), ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("M,H,I", [(8, 1024, 3072), (16, 1024, 3072), (3, 1024, 2048), (8, 2048, 6144)])
-def test_mlp_decode_fused(M, H, I):
-    """Fused decode MLP (one launch, deterministic cross-block reduction) == the two-GEMV path
-    (gate/up + SwiGLU to bf16, down + residual) to fp32 summation order; bit-reproducible across launches
-    (counters re-armed), no arrival timeout."""
-    from qwen_tts import kernels as Kn, _hip
-    dev = _dev()
-    g = torch.Generator().manual_seed(M + H + I)
-    gamma = 1 + 0.1 * torch.randn(H, generator=g)
-    gate, up = torch.randn(I, H, generator=g) * 0.03, torch.randn(I, H, generator=g) * 0.03
-    down = torch.randn(H, I, generator=g) * 0.03
-    tgu = Kn.tile_swiglu(gate.to(dev), up.to(dev), torch.bfloat16, gamma=gamma.to(dev))
-    td = Kn.tile_linear(down.to(dev), torch.bfloat16)
-    ws = torch.zeros(Kn.mlp_ws_bytes(M, H, I), dtype=torch.uint8, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    for it in range(3):
-        x0 = torch.randn(M, H, generator=g).to(dev)
-        h = torch.zeros(M, I, dtype=torch.bfloat16, device=dev)
-        ref = x0.clone()
-        Kn.gemm(x0, tgu, h, M, H, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU, splitk=1)
-        Kn.gemm(h, td, ref, M, I, H, epi=_hip.EPI_ADD, splitk=1)
-        outs = []
-        for _ in range(2):
-            x = x0.clone()
-            Kn.mlp_decode(x, M, H, I, tgu, td, 1e-6, ws, err)
-            outs.append(x)
-        assert torch.equal(outs[0], outs[1])
-        torch.testing.assert_close(outs[0], ref, atol=2e-4, rtol=2e-4)
-    assert int(err.item()) == 0
-
-
 def _bf(t):
     return t.to(torch.bfloat16).float()
 
@@ -1068,9 +1037,13 @@ def test_codec_stream_matches_forward(preset, dtype):
     assert torch.equal(pcms[1], pcms[2])  # captured replay == the eager feed it was captured from
 
 
-@pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice")])
+@pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice"),
+                                           ("codec_full_chunks.npz", "1.7b-customvoice")])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_codec_decode_matches_reference(fname, preset, dtype):
+    """Qwen3TTSTokenizer.decode vs the reference's decode (Z:259-365, K:992-1022) on the same codes: single, ragged
+    batches, and at full dims T = 300 (one chunk), 325 and 700 (300/25 chunk restarts, K:885-895) plus a ragged pair
+    whose long row restarts while the short one is zero padding."""
     from oracle import codec_param_specs, load_preset, synth_state_dict
     from qwen_tts import Qwen3TTSTokenizer
     _dev()
@@ -1086,7 +1059,7 @@ def test_codec_decode_matches_reference(fname, preset, dtype):
         for j, w in enumerate(wavs):
             assert w.shape[0] == int(z[f"{key}/len{j}"]), key
             ref = z[f"{key}/wav{j}"] if f"{key}/wav{j}" in z.files else None
-            got = w if ref is not None else w[::7]
+            got = w if ref is not None else w[::int(z[f"{key}/stride"]) if f"{key}/stride" in z.files else 7]
             ref = ref if ref is not None else z[f"{key}/wav{j}_stride"]
             if dtype == "fp32":
                 np.testing.assert_allclose(got, ref, atol=2e-4, rtol=0, err_msg=key)
@@ -1095,81 +1068,47 @@ def test_codec_decode_matches_reference(fname, preset, dtype):
                 assert rel < 5e-2, (key, rel)
 
 
-@pytest.mark.parametrize("M,N3", [(8, 4096), (8, 2048), (5, 4096), (16, 4096), (1, 2048), (16, 2048)])
-def test_cp_mlp_matches_gemv_chain(M, N3):
-    """qt_cp_mlp (persistent launch: gate/up + SwiGLU -> down + residual -> next RMS GEMV, in-launch tagged hand-offs)
-    == the three decode GEMVs it replaces (same bf16 operand roundings; fp32 summation order differs), over
-    consecutive launches with increasing tags, and no hand-off time-out."""
-    from qwen_tts import kernels as Kn, _hip
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_codec_stream_chunk_restarts_full_dims(dtype):
+    """The streaming codec's chunk handling at full dims (what stream() does per reference chunk: a fresh stateful
+    decoder per 300-frame chunk, primed with the chunk's 25 context frames, fed in pieces, its 555-sample tail
+    dropped at the chunk end) reproduces the reference's chunked decode of 325 and 700 frames (codec_full_chunks.npz,
+    from the reference's own decode): fp32 within 2e-4, bf16 rel-L2 < 5e-2."""
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts.codec import CodecDecoder
     dev = _dev()
-    H, I = 1024, 3072
-    if not Kn.cp_mlp_supported(M, H, I, N3):
-        pytest.skip("needs >= 256 CUs")
-    g = torch.Generator().manual_seed(M * 31 + N3)
-    gam1, gam2 = 1 + 0.1 * torch.randn(H, generator=g), 1 + 0.1 * torch.randn(H, generator=g)
-    wg, wu = torch.randn(I, H, generator=g) * 0.03, torch.randn(I, H, generator=g) * 0.03
-    wd = torch.randn(H, I, generator=g) * 0.02
-    w3 = torch.randn(N3, H, generator=g) * 0.03
-    gu = Kn.tile_swiglu(wg.to(dev), wu.to(dev), torch.bfloat16, gamma=gam1.to(dev))
-    dn = Kn.tile_linear(wd.to(dev), torch.bfloat16)
-    t3 = Kn.tile_linear(w3.to(dev), torch.bfloat16, gamma=gam2.to(dev))
-    x0 = torch.randn(M, H, generator=g).to(dev)
-    tags = torch.zeros(Kn.cp_mlp_tags_bytes(H, I), dtype=torch.uint8, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
-    # reference chain (three decode GEMVs), twice in a row
-    xr, x16r = x0.clone(), x0.to(torch.bfloat16)
-    h = torch.empty(M, I, dtype=torch.bfloat16, device=dev)
-    o_ref = []
-    for _ in range(2):
-        Kn.gemm(x16r, gu, h, M, H, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU, splitk=1)
-        Kn.gemm(h, dn, xr, M, I, H, epi=_hip.EPI_ADD, out2=x16r, splitk=1)
-        o = torch.empty(M, N3, device=dev)
-        Kn.gemm(x16r, t3, o, M, H, N3, rms=True, eps=1e-6, splitk=1)
-        o_ref.append(o)
-    xf, x16f = x0.clone(), x0.to(torch.bfloat16)
-    o_f = []
-    for i in range(2):
-        o = torch.empty(M, N3, device=dev)
-        Kn.cp_mlp(x16f, xf, M, H, I, gu, dn, t3, o, 1e-6, tags, ctr, i + 1, err)
-        o_f.append(o)
-    torch.cuda.synchronize()
-    assert int(err.item()) == 0
-    # a different fp32 summation order flips an occasional bf16 rounding of h / x16 (one bf16 ulp): compare in rel-L2
-    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())  # noqa: E731
-    assert rel(xf - x0, xr - x0) < 2e-3, rel(xf - x0, xr - x0)
-    assert rel(x16f, x16r) < 4e-3
-    for a, b in zip(o_f, o_ref):
-        assert rel(a, b) < 1e-2, rel(a, b)
-
-
-def test_cp_mlp_pipeline_tracks_launch_path(monkeypatch):
-    """The opt-in persistent CP MLP (talker.CP_MLP) in the full bf16 frame graph at the 1.7B CP dims: the first frame's
-    greedy codes equal the launch-per-GEMV path's (bf16 summation-order differences may flip a later near-tie of the
-    synthetic weights' flat logits, after which the continuations differ)."""
-    from qwen_tts import talker as T
-    from qwen_tts.model import TTSModel
-    from qwen_tts.weights import read_json, resolve_path, synthetic, talker_specs
-    dev = _dev()
-    d = resolve_path("synthetic:1.7b-customvoice")
-    cfg = read_json(os.path.join(d, "config.json"))
-    W = synthetic(talker_specs(cfg), dev)  # seeded synthetic weights generated on the device
-    ids = [[151644, 77091, 198] + list(range(1000, 1020)) + [151645, 198, 151644, 77091, 198]] * 2
-    kw = dict(input_ids=ids, languages=["english"] * 2, speakers=["vivian"] * 2, non_streaming_mode=False,
-              max_new_tokens=6, do_sample=False, subtalker_dosample=False)
-    out = {}
-    for on in (False, True):
-        monkeypatch.setattr(T, "CP_MLP", on)
-        m = TTSModel(cfg, W, dtype="bf16")
-        if on:
-            assert m.engine.cp_mlp_ok(2)
-        codes, _ = m.generate(**kw)
-        out[on] = codes
-        del m
-        torch.cuda.empty_cache()
-    for a, b in zip(out[False], out[True]):
-        assert a.shape == b.shape
-        assert torch.equal(a[0], b[0])  # later codes may follow a flipped near-tie into a different continuation
+    z = np.load(os.path.join(GOLD, "codec_full_chunks.npz"))
+    _, ccfg = load_preset("1.7b-customvoice")
+    W = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg), threads=16).items()}
+    dec = CodecDecoder(ccfg, W, dtype=dtype, device=str(dev))
+    up = dec.total_upsample
+    for key in ("t325", "t700"):
+        codes = torch.from_numpy(z[f"{key}/codes0"].astype(np.int32))[None].to(dev)
+        T = codes.shape[1]
+        outs, k = [], 0
+        while k * 300 < T:
+            base = k * 300 - (25 if k * 300 - 25 > 0 else 0)
+            end = min((k + 1) * 300, T)
+            cs = dec.stream(1, 325)
+            fed = base
+            for n in (1, 7, 40, 300):  # ragged feeds
+                n = min(n, end - fed)
+                if n > 0:
+                    cs.feed(codes[:, fed:fed + n])
+                    fed += n
+            assert fed == end and cs.ns == up * (end - base) - 555
+            outs.append(cs.pcm[0, (k * 300 - base) * up:cs.ns].clone())
+            cs.close()
+            k += 1
+        w = torch.cat(outs)[:int(z[f"{key}/len0"])].cpu().numpy()
+        assert w.shape[0] == int(z[f"{key}/len0"])
+        stride = int(z[f"{key}/stride"])
+        got, ref = w[::stride], z[f"{key}/wav0_stride"]
+        if dtype == "fp32":
+            np.testing.assert_allclose(got, ref, atol=2e-4, rtol=0, err_msg=key)
+            np.testing.assert_allclose((w.astype(np.float64) ** 2).sum(), z[f"{key}/wav0_sum"][1], rtol=1e-3)
+        else:
+            assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 5e-2, key
 
 
 def _serve_case():
@@ -1257,3 +1196,78 @@ def test_stream_voice_clone_matches_wrapper(tiny_models, frames, both):
         got = np.concatenate(chunks[b])
         assert got.shape == want.shape, (b, got.shape, want.shape)
         np.testing.assert_allclose(got, want, atol=2e-4, rtol=0)
+
+
+def test_prefill_buffers_lru_bounded(tiny_models):
+    """Static prefill buffers are kept for the PREFILL_CACHE most recently used prompt lengths only (LRU): a server
+    seeing many distinct prompt lengths does not grow HBM without bound, and evicted / re-created lengths still
+    decode exactly as before."""
+    from cases import talker_cases
+    from qwen_tts import talker as T
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype="fp32")
+    case = dict(talker_cases()["cv_b1_nonstream"], max_new_tokens=6)
+    first, mem = {}, []
+    for rep in range(2):
+        for n in range(3, 13):  # 10 distinct prompt lengths, each twice (the second use captures a prefill graph)
+            for _ in range(2):
+                c, _ = _run_case(model, "cv_b1_nonstream", dict(case, texts=[n]), 0, cfg)
+                if rep == 0 and n not in first:
+                    first[n] = c
+                else:
+                    assert all(torch.equal(a, b) for a, b in zip(c, first[n])), n
+            torch.cuda.synchronize()
+            mem.append(torch.cuda.memory_allocated())
+        for s in model.engine.all_sessions():
+            assert len(s.prefill) <= T.PREFILL_CACHE
+    assert max(mem[T.PREFILL_CACHE:]) <= mem[T.PREFILL_CACHE - 1] + (16 << 10), mem
+
+
+def test_rope_growth_keeps_captured_graphs_valid(tiny_models):
+    """Growing the talker's RoPE tables (a session with a longer K/V capacity) must not free the tables that graphs
+    captured by pooled sessions still read: B=1, then the tables grow (old memory reused by new allocations), then
+    the same B=1 request replays its captured frame graph -- identical codes."""
+    from cases import talker_cases
+    from qwen_tts.model import TTSModel
+    cfg, W, _ = tiny_models["tiny-customvoice"]
+    model = TTSModel(cfg, W, dtype="fp32")
+    case = dict(talker_cases()["cv_b1_nonstream"], max_new_tokens=20)
+    a, _ = _run_case(model, "cv_b1_nonstream", case, 0, cfg)
+    t = model.engine.talker
+    old = t.cos.data_ptr()
+    t.ensure_rope(t.cos.shape[0] * 3, model.engine.dev)
+    assert t.cos.data_ptr() != old
+    torch.cuda.empty_cache()
+    junk = [torch.full((1 << 20,), 7.0, device="cuda") for _ in range(16)]  # would land on freed tables
+    b, _ = _run_case(model, "cv_b1_nonstream", case, 0, cfg)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    del junk
+
+
+def test_codec_feed_graph_uses_slot_workspace():
+    """A feed captured on a pooled stream slot while the caller had a temporary split-K workspace active (the
+    voice-clone side-stream feed) must not bind that temporary: every feed of a slot uses the slot's own workspace,
+    so later replays stay correct after the temporary is freed (B=1 -> skinny GEMVs use split-K)."""
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import kernels as Kn
+    from qwen_tts.codec import CodecDecoder
+    dev = _dev()
+    _, ccfg = load_preset("tiny-customvoice")
+    W = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    dec = CodecDecoder(ccfg, W, dtype="fp32", device=str(dev))
+    g = torch.Generator().manual_seed(9)
+    codes = torch.randint(1, dec.tables.shape[1], (1, 12, dec.tables.shape[0]), generator=g).to(dev, torch.int32)
+    ref = dec.forward(codes)
+    for rep in range(4):
+        with Kn.use_workspace(Kn.new_workspace(dev)):
+            cs = dec.stream(1, 12)
+            cs.feed(codes[:, :4])
+            cs.feed(codes[:, 4:12])
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        junk = [torch.full((1 << 20,), 3, dtype=torch.int32, device=dev) for _ in range(8)]  # reuse freed memory
+        torch.testing.assert_close(cs.pcm[:, :cs.ns], ref[:, :cs.ns], atol=2e-5, rtol=0)
+        assert rep < 2 or len(cs.slot.graphs) == 2
+        cs.close()
+        del junk

@@ -78,7 +78,8 @@ def test_oracle_eos_ragged_matches_reference(tiny_talkers):
         np.testing.assert_array_equal(c.numpy(), z[f"eos_b2/codes{j}"])
 
 
-@pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice")])
+@pytest.mark.parametrize("fname,preset", [("codec_tiny.npz", "tiny-customvoice"), ("codec_full.npz", "1.7b-customvoice"),
+                                           ("codec_full_chunks.npz", "1.7b-customvoice")])
 def test_oracle_codec_matches_reference(fname, preset):
     z = np.load(os.path.join(GOLD, fname))
     _, ccfg = load_preset(preset)
@@ -93,7 +94,28 @@ def test_oracle_codec_matches_reference(fname, preset):
             if f"{key}/wav{j}" in z.files:
                 np.testing.assert_allclose(w, z[f"{key}/wav{j}"], atol=2e-5, rtol=0)
             else:
-                np.testing.assert_allclose(w[::7], z[f"{key}/wav{j}_stride"], atol=2e-5, rtol=0)
+                stride = int(z[f"{key}/stride"]) if f"{key}/stride" in z.files else 7
+                np.testing.assert_allclose(w[::stride], z[f"{key}/wav{j}_stride"], atol=2e-5, rtol=0)
                 s = z[f"{key}/wav{j}_sum"]
                 np.testing.assert_allclose([w.astype(np.float64).sum(), (w.astype(np.float64) ** 2).sum()], s,
                                            rtol=1e-4)
+
+
+@pytest.mark.parametrize("key", ["cv06_b1_nonstream"] + (["cv17_b8_stream"] if os.environ.get("QT_SLOW") else []))
+def test_oracle_full_dims_matches_reference(key):
+    """Full ASSUMED dims (configs[1] shape; configs[2] with QT_SLOW=1, ~4 min): the oracle's greedy codes equal the
+    reference's (tests/golden/full_<key>.npz) and its recorded top-2 margins are the fixture's."""
+    from cases import full_cases, make_inputs, margins_grid
+    case = full_cases()[key]
+    cfg, _ = load_preset(case["preset"])
+    z = np.load(os.path.join(GOLD, f"full_{key}.npz"))
+    o = TalkerOracle(cfg, synth_state_dict(talker_param_specs(cfg), threads=8))
+    ids, ins, vcp, ref_ids = make_inputs(case, case["idx"], cfg["talker_config"]["hidden_size"])
+    emb, mask, trail, pad = build_prompts(o, ids, case["languages"], case["speakers"], ins, case["non_streaming_mode"],
+                                          vcp, ref_ids)
+    with torch.no_grad():
+        res = generate(o, emb, mask, trail, pad, record_margins=True, **gen_kwargs(case))
+    for j, c in enumerate(res.codes):
+        np.testing.assert_array_equal(c.numpy(), z[f"codes{j}"])
+    np.testing.assert_allclose(margins_grid(res.margins, len(res.codes), res.raw_tokens.shape[1]), z["margins"],
+                               rtol=1e-5, atol=1e-7)
