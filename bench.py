@@ -27,6 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "qwen3-tts_amd"))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 
 
 def synth_ids(n, seed):
@@ -62,6 +63,118 @@ def gateup_bytes(eng, B):
     L = t.layers[0].gu
     a_bytes = 2 if eng.wdt == torch.bfloat16 else 4
     return L.w.numel() * L.w.element_size() + B * t.H * a_bytes + B * t.I * L.w.element_size()
+
+
+def _graph_us(run, dev, reps=10):
+    """Capture run() into a HIP graph on a side stream, replay it `reps` times between HIP events recorded on that
+    stream; returns microseconds per replay (the per-launch dispatch gaps of the graph included)."""
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        run()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            run()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            g.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def frame_bytes(cfg, B, L_talker):
+    """Algorithmic HBM bytes of one AR frame for B rows at talker cache length L_talker: every
+    talker weight once (28 layers + codec_head), per code-predictor forward (the 2-token prefill + 14 decode steps =
+    15) the 5 layers + that step's lm_head, small_to_mtp once, the talker K/V of every row (28 x 2 x Hkv x D x 2 x L)
+    and the code predictor's K/V (keys 2..16 over the 15 forwards)."""
+    t, c = cfg["talker_config"], cfg["talker_config"]["code_predictor_config"]
+
+    def layer_params(d):
+        H, I, hq, hkv, D = d["hidden_size"], d["intermediate_size"], d["num_attention_heads"], d["num_key_value_heads"], \
+            d["head_dim"]
+        return H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I
+    w_t = t["num_hidden_layers"] * layer_params(t) + t["vocab_size"] * t["hidden_size"]
+    w_cp = c["num_hidden_layers"] * layer_params(c) + c["vocab_size"] * c["hidden_size"]
+    s2m = t["hidden_size"] * c["hidden_size"] if t["hidden_size"] != c["hidden_size"] else 0
+    kv_t = t["num_hidden_layers"] * 2 * t["num_key_value_heads"] * t["head_dim"] * 2 * L_talker
+    kv_cp = sum(c["num_hidden_layers"] * 2 * c["num_key_value_heads"] * c["head_dim"] * 2 * j for j in range(2, 17))
+    return 2 * (w_t + 15 * w_cp + s2m) + B * (kv_t + kv_cp)
+
+
+def whole_frame_roofline(tts, cfg, B, reps=32):
+    """The captured per-frame graph (15 code-predictor steps + the talker step + token choices) of the bench's own
+    session replayed `reps` times at its final cache length: algorithmic bytes per frame / time per frame."""
+    eng = tts.model.engine
+    ss = [s for s in eng.all_sessions() if s.B == B and s.graph is not None and s.force is None]
+    if not ss:
+        return None
+    s = max(ss, key=lambda x: int(x.meta["kv_pos"].max().item()))
+    L = int(s.meta["kv_pos"].max().item()) + 1
+    st = torch.cuda.Stream(device=eng.dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        s.graph.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            s.graph.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    byt = frame_bytes(cfg, B, L)
+    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, keys=L)
+
+
+def attn_oproj_roofline(tts, B, pos=9, reps=20):
+    """Code-predictor fused attention + o_proj + residual (attn_oproj_k) at cache position `pos` (the mean over the
+    15 steps), 5 launches over the 5 layers' distinct o_proj weights per replay.  Algorithmic bytes per launch =
+    o_proj weights + K/V of (pos + 1) keys + the q/k/v rows read + the residual read and written (fp32 + bf16)."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    c, dev = eng.cp, eng.dev
+    kc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    vc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    qkv = torch.randn(B, c.qkv_w, device=dev)
+    x = torch.randn(B, c.H, device=dev)
+    x16 = x.to(torch.bfloat16) if eng.wdt == torch.bfloat16 else None
+
+    def run():
+        for i, L in enumerate(c.layers):
+            Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18,
+                                 L.o, x, const_pos=pos, x16=x16)
+    us = _graph_us(run, dev, reps) / len(c.layers)
+    L0 = c.layers[0]
+    byt = (L0.o.w.numel() * L0.o.w.element_size() + B * c.Hkv * (pos + 1) * c.D * 2 * kc[0].element_size()
+           + B * c.qkv_w * 4 + B * c.H * (4 + 4 + (2 if x16 is not None else 0)))
+    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9)
+
+
+def prefill_mfma(tts, M=680, reps=3):
+    """Prefill linears on gemm_pf_k at M rows (M = 680: four ~170-token voice-clone prompts, configs[4]): per replay
+    the 28 talker layers' q/k/v (RMS), o_proj (+ residual, bf16 shadow), gate/up (RMS, SwiGLU) and down (+ residual)
+    GEMMs on their distinct weights, as _Stack.forward issues them for a prefill.  flops = 2 M sum(N K)."""
+    from qwen_tts import _hip, kernels as Kn
+    eng = tts.model.engine
+    t, dev = eng.talker, eng.dev
+    x = torch.randn(M, t.H, device=dev)
+    x16 = x.to(torch.bfloat16)
+    qkv = torch.empty(M, t.qkv_w, device=dev)
+    att = torch.randn(M, t.Hq * t.D, device=dev).to(eng.wdt)
+    h = torch.empty(M, t.I, dtype=eng.wdt, device=dev)
+
+    def run():
+        for L in t.layers:
+            Kn.gemm(x16, L.qkv, qkv, M, t.H, t.qkv_w, rms=True, eps=t.eps)
+            Kn.gemm(att, L.o, x, M, t.Hq * t.D, t.H, epi=_hip.EPI_ADD, out2=x16)
+            Kn.gemm(x16, L.gu, h, M, t.H, t.I, rms=True, eps=t.eps, epi=_hip.EPI_SWIGLU)
+            Kn.gemm(h, L.down, x, M, t.I, t.H, epi=_hip.EPI_ADD, out2=x16)
+    us = _graph_us(run, dev, reps)
+    nk = t.H * t.qkv_w + t.Hq * t.D * t.H + t.H * 2 * t.I + t.I * t.H
+    flops = 2.0 * M * nk * len(t.layers)
+    return dict(us_per_layer=us / len(t.layers), tflops=flops / (us * 1e-6) / 1e12, M=M)
 
 
 def kernel_roofline(tts, B, reps=10):
@@ -140,6 +253,10 @@ def attention_roofline(tts, B, L, reps=10):
     return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, keys=L)
 
 
+def eng_wdt_bf16(tts):
+    return tts.model.engine.wdt == torch.bfloat16
+
+
 def cpu_baseline(B, prompt, frames, threads):
     """Oracle (CPU fp32 restatement of the reference) on a bounded sample of the same workload."""
     from oracle import CodecOracle, TalkerOracle, build_prompts, codec_param_specs, generate, load_preset
@@ -179,7 +296,13 @@ def main():
     ap.add_argument("--roofline", type=int, default=1)
     ap.add_argument("--row-groups", type=int, default=1,
                     help="decode the per-GPU batch as this many concurrent row groups (streams)")
+    ap.add_argument("--workload", default="cv8", choices=["cv8", "vd64"],
+                    help="cv8: configs[2] (default, weak scaling: 8 x 200-token CustomVoice utterances per GPU); vd64: "
+                         "configs[3] (strong scaling: 64 mixed-length VoiceDesign requests LPT-sharded over the ranks)")
+    ap.add_argument("--slots", type=int, default=64, help="vd64: continuously refilled batch rows per GPU")
     a = ap.parse_args()
+    if a.workload == "vd64":
+        return main_vd64(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -244,6 +367,7 @@ def main():
     value = audio / dt
     # talker cache length at the end of a timed step (prompt + frames), before stream() reuses the sessions
     L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine.all_sessions())
+    fr = whole_frame_roofline(tts, cfg, B) if a.roofline and rank == 0 else None
     # first packet (SURVEY §8 metric): request submit -> first PCM chunk delivered by stream(), p50 of 3 after a
     # warmup, on this rank's batch of B and on a single utterance
     def first_packet(n):
@@ -257,17 +381,45 @@ def main():
     for n in (B, 1):
         first_packet(n)
         fp[n] = 1e3 * float(np.median([first_packet(n) for _ in range(3)]))
-    roof = attn_roof = None
+    roof = attn_roof = frame_roof = ao_roof = pf_roof = None
+    from qwen_tts import _hip
     if a.roofline and rank == 0:
         r = kernel_roofline(tts, B)
-        traffic = None
-        pmcs = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_gateup.json"))
-        if pmcs:  # the newest round's PMC traffic of this kernel (tools/pmc_gateup.py + tools/pmc_reduce.py)
-            traffic = json.load(open(os.path.join(REPO, "profiles", pmcs[-1]))).get("hbm_bytes_per_launch")
+        # HBM traffic of this kernel from rocprofv3 PMC counters (FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected:
+        # tools/pmc_gateup.py + tools/pmc_reduce.py); counters cannot be read inside this process, so the value comes
+        # from the committed profile whose build id (content digest of the kernel sources) matches this library's
+        traffic, tsrc = None, None
+        pdir = os.path.join(REPO, "profiles")
+        pmcs = [f for f in sorted(os.listdir(pdir), reverse=True) if f.endswith("_pmc_gateup.json")]
+        for f in pmcs:
+            j = json.load(open(os.path.join(pdir, f)))
+            if j.get("build_id") == _hip.BUILD_ID:
+                traffic, tsrc = j.get("hbm_bytes_per_launch"), f"profiles/{f} (this build, {j['build_id']})"
+                break
+        if tsrc is None and pmcs:  # newest profile of an earlier build of the kernels: labelled as such
+            j = json.load(open(os.path.join(pdir, pmcs[0])))
+            traffic = j.get("hbm_bytes_per_launch")
+            tsrc = f"profiles/{pmcs[0]} (earlier build {j.get('build_id')}, not this library's {_hip.BUILD_ID})"
         roof = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),
+                "traffic_source": tsrc, "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),
                 "timed_launches": r["launches"]}
+        if fr is not None:
+            frame_roof = {"bound": "hbm", "what": f"whole AR frame (15 CP steps + talker step), B={B}, "
+                                                  f"{fr['keys']} talker keys, captured frame graph replayed",
+                          "achieved": round(fr["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(fr["gbs"] / HBM_PEAK_GBS, 4), "us_per_frame": round(fr["avg_us"], 1),
+                          "bytes_per_frame": int(fr["bytes"])}
+        ao = attn_oproj_roofline(tts, B)
+        ao_roof = {"bound": "hbm", "kernel": f"attn_oproj_k (code-predictor attention + o_proj + residual, B={B}, "
+                                             "10 keys)", "achieved": round(ao["gbs"], 1), "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": round(ao["gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(ao["avg_us"], 2),
+                   "bytes_per_launch": int(ao["bytes"])}
+        if eng_wdt_bf16(tts):
+            pf = prefill_mfma(tts)
+            pf_roof = {"bound": "mfma", "kernel": f"gemm_pf_k (talker prefill linears, M={pf['M']} rows, 28 layers)",
+                       "achieved": round(pf["tflops"], 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                       "frac": round(pf["tflops"] / MFMA_BF16_PEAK_TFS, 4), "us_per_layer": round(pf["us_per_layer"], 1)}
         # decode attention at the run's mean cache length (prompt + half the frames)
         L_mean = max(L_end - a.frames // 2, 1)
         ra = attention_roofline(tts, B, L_mean)
@@ -291,7 +443,99 @@ def main():
                "rtf_per_utterance": round(per_utt_rtf, 2),
                "first_packet_p50_ms": round(fp[B], 1), "first_packet_p50_ms_b1": round(fp[1], 1),
                "full_batch_latency_p50_ms": round(1e3 * float(np.median(lat)), 1),
-               "roofline": roof, "decode_attention_roofline": attn_roof, "cpu_baseline": cpu}
+               "roofline": roof, "decode_attention_roofline": attn_roof, "frame_roofline": frame_roof,
+               "attn_oproj_roofline": ao_roof, "prefill_mfma": pf_roof, "cpu_baseline": cpu,
+               "build_id": _hip.BUILD_ID}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def vd64_requests(n=64, seed=4321):
+    """configs[3]: 64 VoiceDesign requests, text ~ U[40, 300] tokens, instruct ~ U[10, 60] tokens,
+    F ~ U[64, 320] frames, the same list on every rank."""
+    g = np.random.default_rng(seed)
+    texts = g.integers(40, 301, n)
+    ins = g.integers(10, 61, n)
+    frames = g.integers(64, 321, n)
+    ids = [synth_ids(int(t), 5000 + i) for i, t in enumerate(texts)]
+    ins_ids = []
+    for i, k in enumerate(ins):
+        gi = np.random.default_rng([seed, i, 11])
+        ins_ids.append(torch.tensor([[151644, 872, 198] + gi.integers(1000, 150000, int(k)).tolist() + [151645, 198]],
+                                    dtype=torch.long))
+    langs = (["english", "chinese", "japanese", "korean"] * (n // 4 + 1))[:n]
+    return ids, ins_ids, langs, [int(f) for f in frames]
+
+
+def main_vd64(a):
+    """configs[3]: one step = all 64 requests generated (sampling, exact frame counts) and decoded to PCM.  Each rank
+    decodes its longest-first share (qwen_tts.dp.dp_generate: continuous batching through --slots rows, its own PCM);
+    value = total audio seconds of the 64 / max-over-ranks wall time (strong scaling)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if os.environ.get("QT_BENCH_SAME_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("QT_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    from qwen_tts import Qwen3TTSModel, _hip
+    from qwen_tts.dp import dp_generate
+    preset = "1.7b-voicedesign"
+    cfg, W, CW = make_weights(preset, dev, world, rank)
+    tts = Qwen3TTSModel.from_pretrained(f"synthetic:{preset}", device_map=str(dev),
+                                        dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32,
+                                        weights=W, codec_weights=CW)
+    del W, CW
+    torch.cuda.empty_cache()
+    ids, ins_ids, langs, frames = vd64_requests()
+    gen = dict(max_new_tokens=max(frames) + 1, do_sample=True, top_k=50, top_p=1.0, temperature=0.9,
+               subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9,
+               repetition_penalty=1.05, ignore_eos=True, non_streaming_mode=True)
+
+    def step(seed):
+        t0 = time.perf_counter()
+        mine = dp_generate(tts.model, ids, langs, None, ins_ids, frames=frames, slots=a.slots, gather=False,
+                           decode=True, seed=seed, **gen)
+        torch.cuda.synchronize()
+        audio = sum(w.shape[0] for _, w in mine.values()) / 24000.0
+        return audio, time.perf_counter() - t0
+
+    for i in range(a.warmup):
+        step(100 + i)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    audio = 0.0
+    for i in range(a.steps):
+        audio += step(i)[0]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        from qwen_tts.dp import reduce_timing
+        dt, audio = reduce_timing(dt, audio, device=dev)
+    if rank == 0:
+        value = audio / dt
+        out = {"metric": "audio-seconds/sec (RTF) + p50 first-packet latency, 1.7B @ batch 1/8, 1->8 GPU",
+               "value": round(value, 3), "unit": "audio-seconds/sec", "n_gpus": world, "steps": a.steps,
+               "warmup": a.warmup, "ms_per_step": round(1e3 * dt / a.steps, 2), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": a.dtype,
+               "data": "synthetic (seeded weights + token ids)",
+               "config": {"workload": "configs[3]: Qwen3-TTS-12Hz-1.7B VoiceDesign, 64 requests (text U[40,300], "
+                                      "instruct U[10,60] tokens, F U[64,320] frames, sampling) LPT-sharded over the "
+                                      f"ranks, {a.slots} refilled rows per GPU, + codec decode",
+                          "global_batch": 64, "frames_total": int(sum(frames)), "parallelism": f"dp{world}"},
+               "build_id": _hip.BUILD_ID}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

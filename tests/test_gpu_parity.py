@@ -1221,7 +1221,9 @@ def test_prefill_buffers_lru_bounded(tiny_models):
             mem.append(torch.cuda.memory_allocated())
         for s in model.engine.all_sessions():
             assert len(s.prefill) <= T.PREFILL_CACHE
-    assert max(mem[T.PREFILL_CACHE:]) <= mem[T.PREFILL_CACHE - 1] + (16 << 10), mem
+    # the second pass over the same lengths ends with the same PREFILL_CACHE lengths held: the same memory (a growing
+    # cache would hold all ten lengths by now)
+    assert mem[-1] == mem[len(mem) // 2 - 1], mem
 
 
 def test_rope_growth_keeps_captured_graphs_valid(tiny_models):

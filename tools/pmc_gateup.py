@@ -27,3 +27,5 @@ for _ in range(3):
         Kn.gemm(x, L.gu, h, B, t.H, t.I, rms=True, eps=t.eps, epi=_hip.EPI_SWIGLU)
 torch.cuda.synchronize()
 print("weight bytes per launch", t.layers[0].gu.w.numel() * 2)
+with open(os.path.join(REPO, "gpurun_out", "pmc_build_id.txt"), "w") as f:
+    f.write(_hip.BUILD_ID or "")

@@ -26,5 +26,6 @@ out = {"kernel": "gemv_wt<bf16,bf16,bf16,4,4,rms> talker gate-up, N=12288 K=2048
        "dispatches": len(fetch), "fetch_size_kib_raw": round(f_kib, 1), "write_size_kib_raw": round(w_kib, 1),
        "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": algo,
        "traffic_over_algorithmic": round(hbm / algo, 4),
-       "correction": "bytes = 2 x FETCH_SIZE(KiB) x 1024 + WRITE_SIZE(KiB) x 1024 (gfx950 FETCH_SIZE half-count)"}
+       "correction": "bytes = 2 x FETCH_SIZE(KiB) x 1024 + WRITE_SIZE(KiB) x 1024 (gfx950 FETCH_SIZE half-count)",
+       "build_id": sys.argv[3] if len(sys.argv) > 3 else None}
 print(json.dumps(out, indent=1))
