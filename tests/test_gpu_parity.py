@@ -224,6 +224,51 @@ def test_igemm_linear_rms_swiglu_bf16(M, H, I):
     torch.testing.assert_close(xr.cpu(), x + _bf(hb.cpu().float()) @ _bf(down).T, atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(2900, 3072, 512, "swiglu"), (2900, 3072, 512, "rms"), (520, 8192, 1024, "rms"),
+                                        (520, 8192, 1024, "add"), (300, 1000, 640, "add"), (300, 1008, 640, "swiglu"),
+                                        (131, 2048, 6144, "add"), (1100, 4096, 512, "rms"), (1300, 2048, 1024, "add")])
+def test_prefill_gemm_pf2_bf16(M, N, K, mode):
+    """Deep-pipelined prefill GEMM (gemm_pf2_k: LDS-DMA operands, NS stages in flight) on bf16 A, every tile
+    configuration the shape rule picks (256 x 128 / 8 waves, 128 x 128 / 8 waves, 128 x 64 / 4 waves), ragged rows /
+    columns:
+    RMSNorm rows from the bf16 A values, SwiGLU epilogue, residual add with the bf16 shadow (out2), vs torch fp32 on
+    the same bf16-rounded operands."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    Af = A.float()
+    rs = torch.rsqrt(Af.pow(2).mean(-1, keepdim=True) + 1e-6)
+    if mode == "swiglu":
+        I = N // 2
+        gate, up = torch.randn(I, K, generator=g) * 0.05, torch.randn(I, K, generator=g) * 0.05
+        gamma = 1 + 0.1 * torch.randn(K, generator=g)
+        t = Kn.tile_swiglu(gate.to(dev), up.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+        out = torch.zeros(M, I, device=dev, dtype=torch.bfloat16)
+        Kn.gemm(A.to(dev), t, out, M, K, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU)
+        ref = torch.nn.functional.silu((Af @ _bf(gate * gamma).T) * rs) * ((Af @ _bf(up * gamma).T) * rs)
+        torch.testing.assert_close(out.float().cpu(), ref, atol=1e-2, rtol=1e-2)
+        return
+    W = torch.randn(N, K, generator=g) * 0.05
+    if mode == "rms":
+        gamma = 1 + 0.1 * torch.randn(K, generator=g)
+        t = Kn.tile_linear(W.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+        out = torch.zeros(M, N, device=dev)
+        Kn.gemm(A.to(dev), t, out, M, K, N, rms=True, eps=1e-6)
+        ref = (Af @ _bf(W * gamma).T) * rs
+        torch.testing.assert_close(out.cpu(), ref, atol=2e-3, rtol=2e-3)
+        return
+    b = torch.randn(N, generator=g) * 0.1
+    t = Kn.tile_linear(W.to(dev), torch.bfloat16, b.to(dev))
+    x0 = torch.randn(M, N, generator=g)
+    out = x0.to(dev).clone()
+    o16 = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+    Kn.gemm(A.to(dev), t, out, M, K, N, epi=_hip.EPI_ADD, out2=o16)
+    ref = x0 + Af @ _bf(W).T + b
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(o16.float().cpu(), _bf(out.cpu()), atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("D,hq,hkv,window", [(128, 16, 8, 0), (16, 4, 2, 0), (64, 4, 4, 5)])
 def test_qkv_post_and_attention(D, hq, hkv, window):
     from qwen_tts import kernels as Kn
