@@ -60,6 +60,15 @@ def full_cases():
         # configs[1]: 0.6B CustomVoice, 1 utterance of 120 text tokens, non-streaming (Identity small_to_mtp, M:1174)
         "cv06_b1_nonstream": dict(preset="0.6b-customvoice", idx=61, texts=[120], languages=["english"],
                                   speakers=["vivian"], non_streaming_mode=True, max_new_tokens=49),
+        # configs[3] shape: 1.7B VoiceDesign, mixed-length texts and instructs (one row without), left-padded batch
+        "vd17_b4_instruct": dict(preset="1.7b-voicedesign", idx=62, texts=[60, 25, 110, 40], instruct=[30, 12, 0, 45],
+                                 languages=["english", "chinese", "auto", "japanese"], speakers=None,
+                                 non_streaming_mode=True, max_new_tokens=25),
+        # configs[4] shape: 1.7B-Base voice clone, one ICL row (40-token reference text, 38 reference frames) and one
+        # x-vector-only row, streaming text (the voice-clone wrapper's default)
+        "base17_b2_clone": dict(preset="1.7b-base", idx=63, texts=[50, 30], languages=["english", "auto"], speakers=None,
+                                icl=[(40, 38, True, False), (20, 25, False, True)], non_streaming_mode=False,
+                                max_new_tokens=25),
     }
 
 

@@ -1,10 +1,14 @@
-"""Production-shape parity: the HIP path at the full ASSUMED dims of BASELINE.json configs[1] and configs[2] against
+"""Production-shape parity: the HIP path at the full ASSUMED dims of BASELINE.json configs[1]-[4] shapes against
 the reference's own greedy codes (tests/golden/full_<case>.npz, written by make_golden.py --only full from
 `Qwen3TTSForConditionalGeneration.generate`, M:2022-2292, on the same seeded weights).
 
   cv17_b8_stream     1.7B CustomVoice, B=8 x 200-token prompts, streaming text, 32 frames (configs[2] shape)
   cv06_b1_nonstream  0.6B CustomVoice, B=1 x 120-token prompt, non-streaming, 48 frames (configs[1]; the
                      code predictor's small_to_mtp_projection is Identity at 0.6B, M:1171-1174)
+  vd17_b4_instruct   1.7B VoiceDesign, B=4 mixed-length texts + instructs (one row without), non-streaming, 24 frames
+                     (configs[3] shape: left-padded batch, instruct prepended, M:2076-2080)
+  base17_b2_clone    1.7B-Base voice clone, one ICL row (40-token reference text, 38 reference frames) and one
+                     x-vector-only row, streaming text, 24 frames (configs[4] shape: M:1968-2019, 2102-2106)
 
 Every greedy pick of the reference (talker cb0 and the code predictor's 15, [B, frames, 16]) carries its top-2
 margin of the processed scores (from the oracle, itself asserted bit-identical to the reference's codes when the
@@ -99,7 +103,10 @@ def _check_free_run(codes, ref, margins, tol, label, require_full=False):
     return div
 
 
-@pytest.mark.parametrize("key", ["cv06_b1_nonstream", "cv17_b8_stream"])
+KEYS = ["cv06_b1_nonstream", "cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone"]
+
+
+@pytest.mark.parametrize("key", KEYS)
 def test_full_dims_fp32_bit_exact(key):
     from qwen_tts.model import TTSModel
     _dev()
@@ -120,7 +127,7 @@ def test_full_dims_fp32_bit_exact(key):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("key", ["cv06_b1_nonstream", "cv17_b8_stream"])
+@pytest.mark.parametrize("key", KEYS)
 def test_full_dims_bf16_teacher_forced(key):
     from cases import first_divergence, gen_kwargs
     from qwen_tts.model import TTSModel

@@ -101,7 +101,8 @@ def test_oracle_codec_matches_reference(fname, preset):
                                            rtol=1e-4)
 
 
-@pytest.mark.parametrize("key", ["cv06_b1_nonstream"] + (["cv17_b8_stream"] if os.environ.get("QT_SLOW") else []))
+@pytest.mark.parametrize("key", ["cv06_b1_nonstream"] + (["cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone"]
+                                           if os.environ.get("QT_SLOW") else []))
 def test_oracle_full_dims_matches_reference(key):
     """Full ASSUMED dims (configs[1] shape; configs[2] with QT_SLOW=1, ~4 min): the oracle's greedy codes equal the
     reference's (tests/golden/full_<key>.npz) and its recorded top-2 margins are the fixture's."""
