@@ -3,7 +3,7 @@ torch.matmul (hipBLASLt, plain bf16 GEMM, no fused prologue / epilogue) on the s
 reaches here is the practical target.  Weights distinct per launch (28 layers' worth), HIP events around graph
 replays.
 
-    python tools/pf_gemm_probe.py [M ...]
+    python tools/pf_gemm_probe.py [M ...]        (QT_PROBE_SHAPES=gate-up,down limits the shapes)
 """
 import os
 import sys
@@ -42,19 +42,23 @@ def main():
     for M in Ms:
         tot_ours = tot_lib = 0.0
         flops_tot = 0.0
+        only = [x for x in os.environ.get("QT_PROBE_SHAPES", "").split(",") if x]
         for name, N, Kk, rms, epi in SHAPES:
+            if only and name not in only:
+                continue
             Wf = [torch.randn(N, Kk, device=dev) * 0.02 for _ in range(nl)]
             Wt = [K.tile_linear(w, torch.bfloat16) for w in Wf]
             Wb = [w.to(torch.bfloat16).t().contiguous() for w in Wf]  # [K][N] for A @ W
             del Wf
-            A = torch.randn(M, Kk, device=dev).to(torch.bfloat16)
+            pad = int(os.environ.get("QT_PROBE_LDA_PAD", "0"))  # A row stride K + pad elements
+            A = torch.randn(M, Kk + pad, device=dev).to(torch.bfloat16)[:, :Kk]
             o = (torch.zeros(M, N // 2, device=dev, dtype=torch.bfloat16) if epi == _hip.EPI_SWIGLU else
                  torch.zeros(M, N, device=dev))
             o16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 
             def ours():
                 for w in Wt:
-                    K.gemm(A, w, o, M, Kk, o.shape[1], rms=rms, eps=1e-6, epi=epi)
+                    K.gemm(A, w, o, M, Kk + pad, o.shape[1], rms=rms, eps=1e-6, epi=epi)
 
             def lib():
                 for w in Wb:
