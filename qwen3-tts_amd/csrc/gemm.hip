@@ -1208,6 +1208,11 @@ void launch_pf2_auto(const GemmP& p, hipStream_t s) {
   else if (cfg == 6) launch_pf2<OT, 256, 16, 2, 2, 4>(p, s);    // 8 waves, 256 x 256, wave tile 128 x 64
   else if (cfg == 7) launch_pf2<OT, 256, 8, 3, 4, 2, false>(p, s);  // cfg 4 with fragment-order A (A/B)
   else if (cfg == 8) launch_pf2<OT, 128, 4, 3, 2, 2, false>(p, s);  // cfg 3 with fragment-order A (A/B)
+  else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);    // 4 waves, 256 x 160, wave tile 128 x 80
+  else if (cfg == 10) launch_pf2<OT, 128, 10, 4, 2, 2>(p, s);   // 4 waves, 128 x 160, wave tile 64 x 80
+  else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);     // 4 waves, 64 x 96, wave tile 32 x 48
+  else if (cfg == 12) launch_pf2<OT, 256, 16, 2, 2, 2>(p, s);   // 4 waves, 256 x 256, wave tile 128 x 128
+  else if (cfg == 13) launch_pf2<OT, 128, 8, 4, 2, 2>(p, s);    // 4 waves, 128 x 128, wave tile 64 x 64
   else launch_pf2<OT, 128, 4, 3>(p, s);
 }
 
