@@ -12,33 +12,14 @@
 // * K is split across the block's waves; partial 16x16 tiles are reduced through LDS, then the fused
 //   epilogue (bias, SiLU/GELU, LayerScale, residual add, SwiGLU pairing) writes the output.
 // Decode (M <= 16) is HBM-bound on W: roofline = W bytes / 8 TB/s.
-#include "common.h"
+#include "gemm_p.h"
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
 
 namespace {
 
-struct GemmP {
-  int M, N, Kp, Klog;          // Kp = padded K (taps * cin_pad), Klog = RMSNorm length
-  const void* A; long long lda;
-  const int* a_index;
-  const void* W;
-  const float* gamma; float eps; int rms;
-  const float* bias; const float* colscale;
-  int act, epi;
-  void* out; long long ldo;
-  int taps, dil, cin, cin_pad, t_in, t_out, t_off;
-  int ks;                       // split-K factor (gridDim.y), 1 = none
-  int wpb_max;                  // waves-per-block cap of the decode GEMV (16, or 8 for wide grids)
-  int no_igemm;                 // 1: keep large-M GEMMs on gemm_wt (A/B measurement)
-  int ntl;                      // 1: non-temporal weight loads (decode GEMV over >= 16 MiB of weights)
-  unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
-  const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
-  int a_elu;                    // ELU on A (tokenizer encoder convs)
-  int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))
-  bf16_t* out2; long long ldo2; // optional bf16 copy of the stored output (decode residual stream shadow)
-};
+using qt_gemm_impl::GemmP;
 
 // SnakeBeta exactly as qt_snake computes it (fp32 math on the stored activation)
 QT_DEV float snake1(float v, float al, float ib) {
@@ -821,198 +802,6 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   }
 }
 
-// Prefill linear GEMM, deep pipeline (taps == 0, bf16 A and bf16 pre-tiled W, K % 64 == 0): block tile BM rows x
-// NTB*16 columns, 4 waves in a 2 x 2 grid (wave = BM/2 rows x NTB/2 column tiles of 16x16x32 MFMAs), K in 64-deep
-// stages, NS LDS stages.  Both operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, inline asm, no VGPR
-// staging) and NS - 1 stages are in flight while one is multiplied: a counted `s_waitcnt vmcnt` retires exactly the
-// stage about to be read and a raw `s_barrier` (no vmcnt(0) drain) publishes it (cdna_hip_programming.md §5
-// "Pipelining across barriers").  gemm_pf_k (one stage of register-staged prefetch) left each 512-cycle MFMA stage
-// waiting on the next stage's L2/HBM round trip: M=680 talker layer 293 us = 234 TFLOP/s, hipBLASLt 130 us
-// (tools/pf_gemm_probe.py).
-// LDS images are lane-linear 1 KiB fragments, exactly the MFMA operand order: B fragments are the pre-tiled weight
-// tiles copied verbatim (1 KiB contiguous per DMA instruction); an A fragment (16 rows x 32 k) is gathered by one DMA
-// instruction whose lane j reads row j & 15, k chunk j >> 4 (16 rows x 64 B), so every ds_read_b128 of an operand is
-// conflict-free.  The RMSNorm sums of squares come from the A fragments the MFMA reads (column-half-0 waves).
-// Blocks are remapped so the row tiles of one column tile are dealt to one XCD (its weight slice is fetched into one
-// L2 once, speed only).  Same operand rounding and per-element k order as gemm_pf_k / igemm_k.
-QT_DEV void glds16(const void* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-QT_DEV unsigned lds_u32(const void* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
-}
-template <int N> QT_DEV void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-QT_DEV void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
-template <int I, int N, typename F>
-QT_DEV void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
-  constexpr int NW = WM * WN;
-  constexpr int MI = BM / WM / 16;            // row fragments per wave
-  constexpr int CT = NTB / WN;                // column tiles per wave
-  constexpr int A_FR = BM / 8, B_FR = NTB * 2;  // 1 KiB fragments per stage
-  constexpr int STAGE = (A_FR + B_FR) * 512;  // bf16 elements per stage
-  constexpr int GA = A_FR / NW, GB = B_FR / NW, G = GA + GB;  // DMA instructions per wave per stage
-  static_assert(A_FR % NW == 0 && B_FR % NW == 0 && MI >= 1 && CT >= 1, "fragments split over the waves");
-  __shared__ __attribute__((aligned(16))) bf16_t smem_pf2[NS * STAGE + 2 * BM];  // NS stages, then BM row sums
-  float* ss_row = (float*)(smem_pf2 + NS * STAGE);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lm = lane & 15, lk = lane >> 4;
-  const int ntl = (p.N + 15) / 16, ktiles = p.Kp / 32, S = p.Klog / 64;
-  // XCD-aware tile order: blocks that share an XCD (linear id % 8) take consecutive tiles, row tiles fastest
-  const int mtiles = (p.M + BM - 1) / BM, ctiles = (ntl + NTB - 1) / NTB;
-  const int nwg = mtiles * ctiles, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int m0 = (wg % mtiles) * BM, nt0 = (wg / mtiles) * NTB;
-  const int wr = (w / WN) * (BM / WM), wc = (w % WN) * CT;
-  const bool norm = p.rms != 0;
-  const bf16_t* Ab = (const bf16_t*)p.A;
-  const bf16_t* Wb = (const bf16_t*)p.W;
-  // this lane's DMA sources: A fragment f = w * GA + i covers rows (f >> 1) * 16.., k tile f & 1
-  const int arow = min(m0 + lm, p.M - 1);
-  const unsigned lbase = lds_u32(smem_pf2);
-  auto issue = [&](int st) {
-    const unsigned sb = lbase + (unsigned)((st % NS) * STAGE * 2);
-#pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int f = w * GA + i;
-      if constexpr (AFL) {  // full 128-B lines: piece f = rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
-        const int rr = f * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((rr >> 1) & 7);
-        const int row = min(m0 + rr, p.M - 1);
-        glds16(Ab + (long long)row * p.lda + st * 64 + c * 8, sb + f * 1024);
-      } else {  // MFMA fragment order: 16 rows x 64 B per piece
-        const int mt = f >> 1, kt = f & 1;
-        const int row = min(arow + mt * 16, p.M - 1);
-        glds16(Ab + (long long)row * p.lda + st * 64 + kt * 32 + lk * 8, sb + f * 1024);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < GB; ++i) {
-      const int f = w * GB + i, ct = f >> 1, kt = f & 1;
-      const int nt = min(nt0 + ct, ntl - 1);
-      glds16(Wb + ((size_t)nt * ktiles + st * 2 + kt) * 512 + lane * 8, sb + (A_FR + f) * 1024);
-    }
-  };
-  f32x4_t acc[MI][CT];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float ss[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) ss[i] = 0.f;
-  const bool do_ss = norm && (w % WN) == 0;
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < S) issue(s);
-  for (int s = 0; s < S; ++s) {
-    // retire stage s (this wave's DMAs): the stages issued after it may stay in flight
-    const int after = min(S - 1, s + NS - 2) - s;
-    if constexpr (NS >= 4) { if (after >= 2) vm_wait_n<2 * G>(); else if (after == 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
-    else { if (after >= 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
-    raw_barrier();  // every wave's stage-s DMAs landed; every wave is done reading stage s - 1's buffer
-    if (s + NS - 1 < S) issue(s + NS - 1);
-    const bf16_t* sa = smem_pf2 + (s % NS) * STAGE;
-    const bf16_t* sbf = sa + A_FR * 512;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4_t af[MI], bfr[CT];
-#pragma unroll
-      for (int j = 0; j < CT; ++j) bfr[j] = *(const u32x4_t*)(sbf + ((wc + j) * 2 + kk) * 512 + lane * 8);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        if constexpr (AFL) af[i] = *(const u32x4_t*)(sa + (wr + i * 16 + lm) * 64 + (((kk * 4 + lk) ^ (lm >> 1)) * 8));
-        else af[i] = *(const u32x4_t*)(sa + ((wr / 16 + i) * 2 + kk) * 512 + lane * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < CT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
-                                                              __builtin_bit_cast(bf16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
-      if (do_ss) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float lo = __uint_as_float(af[i][e] << 16), hi = __uint_as_float(af[i][e] & 0xFFFF0000u);
-            ss[i] += lo * lo + hi * hi;
-          }
-      }
-    }
-  }
-  if (norm) {  // row sums: lanes l, l^16, l^32, l^48 hold the four k chunks of row l & 15
-    if (do_ss) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        float v = ss[i] + xor_lane<16>(ss[i]);
-        v += xor_lane<32>(v);
-        if (lane < 16) ss_row[wr + i * 16 + lane] = v;
-      }
-    }
-    __syncthreads();  // (no DMA in flight any more)
-  }
-  OT* out = (OT*)p.out;
-  // epilogue per accumulator tile; indices are compile-time (static_for), so the accumulators stay in registers
-  auto epi = [&](const f32x4_t a, const int i, const int qd) {
-    const int nt = nt0 + wc + qd;
-    if (nt >= ntl) return;
-    const int n = nt * 16 + lm;
-    const bool nval = n < p.N;
-    const float bias = (p.bias && nval) ? p.bias[n] : 0.f;
-    const float cs = (p.colscale && nval) ? p.colscale[n] : 1.f;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int rl = wr + i * 16 + lk * 4 + e;
-      float x = a[e];
-      if (norm) x *= rsqrtf(ss_row[rl] / (float)p.Klog + p.eps);
-      x += bias;
-      if (p.act != QT_ACT_NONE) x = act_f_call(x, p.act);
-      v[e] = x * cs;
-    }
-    if (p.epi == QT_EPI_SWIGLU) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float up = __shfl_xor(v[e], 8, 64);
-        const int m = m0 + wr + i * 16 + lk * 4 + e;
-        if (lm < 8 && m < p.M && nt * 8 + lm < (p.N >> 1))
-          out[(long long)m * p.ldo + nt * 8 + lm] = from_f<OT>(silu_f(v[e]) * up);
-      }
-      return;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + wr + i * 16 + lk * 4 + e;
-      if (m >= p.M || !nval) continue;
-      OT* o = out + (long long)m * p.ldo + n;
-      const float r = p.epi == QT_EPI_ADD ? to_f(*o) + v[e] : v[e];
-      *o = from_f<OT>(r);
-      if (p.out2) p.out2[(long long)m * p.ldo2 + n] = f2bf(r);
-    }
-  };
-  static_for<0, MI * CT>([&](auto I) {
-    constexpr int i = decltype(I)::value / CT, qd = decltype(I)::value % CT;
-    epi(acc[i][qd], i, qd);
-  });
-}
-
-template <typename OT, int BM, int NTB, int NS, int WM = 2, int WN = 2, bool AFL = true>
-void launch_pf2(const GemmP& p, hipStream_t s) {
-  const int ntl = (p.N + 15) / 16;
-  const int nwg = ((p.M + BM - 1) / BM) * ((ntl + NTB - 1) / NTB);
-  hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL>), dim3(nwg), dim3(WM * WN * 64), 0, s, p);
-}
 
 // Single-output-channel causal conv (codec conv_last, Cout = 1): memory-bound, so no MFMA.  A block owns
 // 256 consecutive outputs of one batch item; the input window (256 + (taps-1)*dil rows) x 32 channels is staged
@@ -1180,41 +969,12 @@ bool pf_route(const GemmP& p) {
          p.sn_a == nullptr && !p.no_igemm;
 }
 
-// gemm_pf2_k (deep-pipelined LDS-DMA prefill GEMM): QT_PF2=0 keeps gemm_pf_k (A/B); QT_PF2_CFG = 1..3 forces a tile
-// (1: 256 x 128, 2: 128 x 128, 3: 128 x 64) for measurement, 0 = chosen by shape
+// gemm_pf2_k (deep-pipelined LDS-DMA prefill GEMM, gemm_pf2.hip): QT_PF2=0 keeps gemm_pf_k (A/B)
 inline int pf2_mode() {
   static const int v = [] { const char* e = getenv("QT_PF2"); return e ? atoi(e) : 1; }();
   return v;
 }
-inline int pf2_cfg() {
-  static const int v = [] { const char* e = getenv("QT_PF2_CFG"); return e ? atoi(e) : 0; }();
-  return v;
-}
 
-// Tile rule from tools/pf_gemm_probe.py on the 1.7B talker shapes (profiles/r03_pf2_gemm_probe.txt): 256 x 128 with 8
-// waves once M >= 1024 gives >= 200 blocks of it, else 128 x 128 with 8 waves at >= 200 blocks, else 128 x 64 with 4
-// waves (M = 680 layer 293 -> 247 us, M = 1600 396 -> 346, M = 4096 736 -> 667 against gemm_pf_k).
-template <typename OT>
-void launch_pf2_auto(const GemmP& p, hipStream_t s) {
-  const int ntl = (p.N + 15) / 16;
-  const long long b4 = (long long)((p.M + 255) / 256) * ((ntl + 7) / 8);
-  const long long b5 = (long long)((p.M + 127) / 128) * ((ntl + 7) / 8);
-  int cfg = pf2_cfg();
-  if (cfg == 0) cfg = (p.M >= 1024 && b4 >= 200) ? 4 : ((p.M >= 1024 && b5 >= 200) ? 5 : 3);
-  if (cfg == 1) launch_pf2<OT, 256, 8, 3>(p, s);
-  else if (cfg == 2) launch_pf2<OT, 128, 8, 4>(p, s);
-  else if (cfg == 4) launch_pf2<OT, 256, 8, 3, 4, 2>(p, s);     // 8 waves, wave tile 64 x 64
-  else if (cfg == 5) launch_pf2<OT, 128, 8, 3, 2, 4>(p, s);     // 8 waves, wave tile 64 x 32
-  else if (cfg == 6) launch_pf2<OT, 256, 16, 2, 2, 4>(p, s);    // 8 waves, 256 x 256, wave tile 128 x 64
-  else if (cfg == 7) launch_pf2<OT, 256, 8, 3, 4, 2, false>(p, s);  // cfg 4 with fragment-order A (A/B)
-  else if (cfg == 8) launch_pf2<OT, 128, 4, 3, 2, 2, false>(p, s);  // cfg 3 with fragment-order A (A/B)
-  else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);    // 4 waves, 256 x 160, wave tile 128 x 80
-  else if (cfg == 10) launch_pf2<OT, 128, 10, 4, 2, 2>(p, s);   // 4 waves, 128 x 160, wave tile 64 x 80
-  else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);     // 4 waves, 64 x 96, wave tile 32 x 48
-  else if (cfg == 12) launch_pf2<OT, 256, 16, 2, 2, 2>(p, s);   // 4 waves, 256 x 256, wave tile 128 x 128
-  else if (cfg == 13) launch_pf2<OT, 128, 8, 4, 2, 2>(p, s);    // 4 waves, 128 x 128, wave tile 64 x 64
-  else launch_pf2<OT, 128, 4, 3>(p, s);
-}
 
 template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
@@ -1236,7 +996,8 @@ int launch(const GemmP& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_wt<WT, AT, OT, 1, 8>), dim3(nt, 1), dim3(512), 0, s, p);
   } else if (pf_route<WT, AT>(p) && pf2_mode() && p.Klog % 64 == 0 && p.Kp == p.Klog &&
              ((size_t)p.A & 15) == 0) {
-    launch_pf2_auto<OT>(p, s);
+    if constexpr (std::is_same<OT, float>::value) qt_gemm_impl::launch_pf2_auto_f32(p, s);
+    else qt_gemm_impl::launch_pf2_auto_bf16(p, s);
   } else if (pf_route<WT, AT>(p)) {
     // prefill linears: LDS-staged A and B, 128 x 128 tiles (128 x 64 when that leaves < 256 blocks)
     const int mt = (p.M + PF_BM - 1) / PF_BM;

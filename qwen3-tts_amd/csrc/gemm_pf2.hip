@@ -1,0 +1,378 @@
+// gemm_pf2_k: the prefill linears' GEMM (talker / code-predictor prefill q/k/v, o_proj, gate/up + SwiGLU, down;
+// codec pre-transformer linears on bf16 activations), routed here by qt_gemm (gemm.hip) for bf16 A + bf16 pre-tiled
+// weights with K % 64 == 0.  Own translation unit so the tile configurations build in parallel with gemm.hip.
+#include "gemm_p.h"
+#include <cstdlib>
+#include <type_traits>
+
+#ifdef QT_PF2_STAMPS  // diagnostic build only (tools/pf2_probe.hip): per-block cycle stamps of wave 0
+__device__ unsigned long long pf2_stamps[1 << 14][4];
+#define PF2_STAMP(k)                                                                            \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < (1 << 14)) pf2_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PF2_STAMP(k) do { } while (0)
+#endif
+
+namespace {
+
+using qt_gemm_impl::GemmP;
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// SiLU from the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each, 4 instructions): the IEEE
+// division + range-reduced expf of silu_f cost ~40 VALU per element, which made the SwiGLU epilogue of a
+// 256 x 160 tile 30k cycles (the output is rounded to bf16 anyway).
+QT_DEV float silu_fast(float g) {
+  return g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * g));
+}
+
+// Prefill linear GEMM, deep pipeline (taps == 0, bf16 A and bf16 pre-tiled W, K % 64 == 0): block tile BM rows x
+// NTB*16 columns, 4 waves in a 2 x 2 grid (wave = BM/2 rows x NTB/2 column tiles of 16x16x32 MFMAs), K in 64-deep
+// stages, NS LDS stages.  Both operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, inline asm, no VGPR
+// staging) and NS - 1 stages are in flight while one is multiplied: a counted `s_waitcnt vmcnt` retires exactly the
+// stage about to be read and a raw `s_barrier` (no vmcnt(0) drain) publishes it (cdna_hip_programming.md §5
+// "Pipelining across barriers").  gemm_pf_k (one stage of register-staged prefetch) left each 512-cycle MFMA stage
+// waiting on the next stage's L2/HBM round trip: M=680 talker layer 293 us = 234 TFLOP/s, hipBLASLt 130 us
+// (tools/pf_gemm_probe.py).
+// LDS images are lane-linear 1 KiB fragments, exactly the MFMA operand order: B fragments are the pre-tiled weight
+// tiles copied verbatim (1 KiB contiguous per DMA instruction); an A fragment (16 rows x 32 k) is gathered by one DMA
+// instruction whose lane j reads row j & 15, k chunk j >> 4 (16 rows x 64 B), so every ds_read_b128 of an operand is
+// conflict-free.  The RMSNorm sums of squares come from the A fragments the MFMA reads (column-half-0 waves).
+// Blocks are remapped so the row tiles of one column tile are dealt to one XCD (its weight slice is fetched into one
+// L2 once, speed only).  Same operand rounding and per-element k order as gemm_pf_k / igemm_k.
+QT_DEV void glds16(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+QT_DEV unsigned lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
+}
+template <int N> QT_DEV void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+QT_DEV void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+template <int I, int N, typename F>
+QT_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// EPI: the epilogue, compile-time for the prefill linears' plain forms (no act / bias / colscale): PF2_STORE,
+// PF2_ADD (residual add), PF2_ADD_OUT2 (+ bf16 shadow), PF2_SWIGLU; PF2_GENERIC reads all of it from GemmP.
+// ABL (measurement only, tools/pf2_probe.hip), bit mask: 1 no MFMA (fragment reads kept live), 2 no loads after the
+// prologue (the rest runs on stale stages), 4 no fragment reads (and no MFMA), 8 no epilogue (accumulators kept live)
+enum { PF2_GENERIC = -1, PF2_STORE = 0, PF2_ADD = 1, PF2_SWIGLU = 2, PF2_ADD_OUT2 = 3 };
+template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL, int EPI, int ABL = 0>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
+  constexpr int NW = WM * WN;
+  constexpr int MI = BM / WM / 16;            // row fragments per wave
+  constexpr int CT = NTB / WN;                // column tiles per wave
+  constexpr int A_FR = BM / 8, B_FR = NTB * 2;  // 1 KiB fragments per stage
+  constexpr int STAGE = (A_FR + B_FR) * 512;  // bf16 elements per stage
+  constexpr int GA = A_FR / NW, GB = B_FR / NW, G = GA + GB;  // DMA instructions per wave per stage
+  static_assert(A_FR % NW == 0 && B_FR % NW == 0 && MI >= 1 && CT >= 1, "fragments split over the waves");
+  // NS stages, then the row sums of squares: WN partial sums per row (one per wave of a row block)
+  __shared__ __attribute__((aligned(16))) bf16_t smem_pf2[NS * STAGE + 2 * WN * BM];
+  float* ss_row = (float*)(smem_pf2 + NS * STAGE);
+  PF2_STAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lm = lane & 15, lk = lane >> 4;
+  const int ntl = (p.N + 15) / 16, ktiles = p.Kp / 32, S = p.Klog / 64;
+  // XCD-aware tile order: blocks that share an XCD (linear id % 8) take consecutive tiles, row tiles fastest
+  const int mtiles = (p.M + BM - 1) / BM, ctiles = (ntl + NTB - 1) / NTB;
+  const int nwg = mtiles * ctiles, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int m0 = (wg % mtiles) * BM, nt0 = (wg / mtiles) * NTB;
+  const int wr = (w / WN) * (BM / WM), wc = (w % WN) * CT;
+  const bool norm = p.rms != 0;
+  const bf16_t* Ab = (const bf16_t*)p.A;
+  const bf16_t* Wb = (const bf16_t*)p.W;
+  // this lane's DMA sources: A fragment f = w * GA + i covers rows (f >> 1) * 16.., k tile f & 1
+  const int arow = min(m0 + lm, p.M - 1);
+  const unsigned lbase = lds_u32(smem_pf2);
+  auto issue = [&](int st) {
+    const unsigned sb = lbase + (unsigned)((st % NS) * STAGE * 2);
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int f = w * GA + i;
+      if constexpr (AFL) {  // full 128-B lines: piece f = rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+        const int rr = f * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((rr >> 1) & 7);
+        const int row = min(m0 + rr, p.M - 1);
+        glds16(Ab + (long long)row * p.lda + st * 64 + c * 8, sb + f * 1024);
+      } else {  // MFMA fragment order: 16 rows x 64 B per piece
+        const int mt = f >> 1, kt = f & 1;
+        const int row = min(arow + mt * 16, p.M - 1);
+        glds16(Ab + (long long)row * p.lda + st * 64 + kt * 32 + lk * 8, sb + f * 1024);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int f = w * GB + i, ct = f >> 1, kt = f & 1;
+      const int nt = min(nt0 + ct, ntl - 1);
+      glds16(Wb + ((size_t)nt * ktiles + st * 2 + kt) * 512 + lane * 8, sb + (A_FR + f) * 1024);
+    }
+  };
+  f32x4_t acc[MI][CT];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // RMSNorm sums of squares from the A fragments the MFMAs read: the WN waves of a row block hold the same
+  // fragments, wave j of them takes the fragment dwords e with e % WN == j (v_dot2 on the bf16 pairs, fp32 sums)
+  float ss[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) ss[i] = 0.f;
+  const int wj = w % WN;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < S) issue(s);
+  for (int s = 0; s < S; ++s) {
+    // retire stage s (this wave's DMAs): the stages issued after it may stay in flight
+    const int after = min(S - 1, s + NS - 2) - s;
+    if constexpr (NS >= 4) { if (after >= 2) vm_wait_n<2 * G>(); else if (after == 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
+    else { if (after >= 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
+    raw_barrier();  // every wave's stage-s DMAs landed; every wave is done reading stage s - 1's buffer
+    if (!(ABL & 2) && s + NS - 1 < S) issue(s + NS - 1);
+    if constexpr ((ABL & 4) != 0) continue;
+    const bf16_t* sa = smem_pf2 + (s % NS) * STAGE;
+    const bf16_t* sbf = sa + A_FR * 512;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4_t af[MI], bfr[CT];
+#pragma unroll
+      for (int j = 0; j < CT; ++j) bfr[j] = *(const u32x4_t*)(sbf + ((wc + j) * 2 + kk) * 512 + lane * 8);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if constexpr (AFL) af[i] = *(const u32x4_t*)(sa + (wr + i * 16 + lm) * 64 + (((kk * 4 + lk) ^ (lm >> 1)) * 8));
+        else af[i] = *(const u32x4_t*)(sa + ((wr / 16 + i) * 2 + kk) * 512 + lane * 8);
+      }
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < CT; ++j) asm volatile("" ::"v"(bfr[j]));
+      } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                              __builtin_bit_cast(bf16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
+      }
+      if (norm) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int e2 = 0; e2 < 4 / WN; ++e2) {
+            unsigned d = af[i][e2 * WN];
+#pragma unroll
+            for (int t = 1; t < WN; ++t) d = wj == t ? af[i][e2 * WN + t] : d;  // wave-uniform select, no branch
+            const bf16x2_t h = __builtin_bit_cast(bf16x2_t, d);
+            ss[i] = __builtin_amdgcn_fdot2_f32_bf16(h, h, ss[i], false);
+          }
+      }
+    }
+  }
+  PF2_STAMP(1);
+  if (norm) {  // row sums: lanes l, l^16, l^32, l^48 hold the four k chunks of row l & 15
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      float v = ss[i] + xor_lane<16>(ss[i]);
+      v += xor_lane<32>(v);
+      if (lane < 16) ss_row[wj * BM + wr + i * 16 + lane] = v;
+    }
+    __syncthreads();  // (no DMA in flight any more)
+  }
+  if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  OT* out = (OT*)p.out;
+  // Epilogue.  Everything a store depends on is loaded before the first store: vmcnt counts loads and stores in
+  // issue order, so a load issued after a store makes its consumer wait for that store's round trip (one per tile
+  // when bias / residual loads were interleaved with the stores).  Interior blocks store without bounds checks, and
+  // the plain forms have no per-element branches (each one had cost an exec-mask branch per element).
+  const float inv_k = 1.f / (float)p.Klog;
+  float rsc[MI][4];  // per-row RMS scale of this lane's rows wr + i*16 + lk*4 + e
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rsc[i][e] = 1.f;
+  if (norm) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      f32x4_t t = *(const f32x4_t*)(ss_row + wr + i * 16 + lk * 4);
+#pragma unroll
+      for (int j = 1; j < WN; ++j) t += *(const f32x4_t*)(ss_row + j * BM + wr + i * 16 + lk * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rsc[i][e] = rsqrtf(t[e] * inv_k + p.eps);
+    }
+  }
+  float cb[CT], cc[CT];  // bias / colscale of this lane's columns (clamped addresses: no branch around a load)
+#pragma unroll
+  for (int q = 0; q < CT; ++q) { cb[q] = 0.f; cc[q] = 1.f; }
+  if constexpr (EPI == PF2_GENERIC) {
+    if (p.bias) {
+#pragma unroll
+      for (int q = 0; q < CT; ++q) cb[q] = p.bias[min((nt0 + wc + q) * 16 + lm, p.N - 1)];
+    }
+    if (p.colscale) {
+#pragma unroll
+      for (int q = 0; q < CT; ++q) cc[q] = p.colscale[min((nt0 + wc + q) * 16 + lm, p.N - 1)];
+    }
+  }
+  const bool add = EPI == PF2_GENERIC ? p.epi == QT_EPI_ADD : (EPI == PF2_ADD || EPI == PF2_ADD_OUT2);
+  const bool swiglu = EPI == PF2_GENERIC ? p.epi == QT_EPI_SWIGLU : EPI == PF2_SWIGLU;
+  // residual rows are loaded RCH row fragments at a time (all of them up to 64 registers)
+  constexpr int RCH = (MI * CT * 4 <= 64) ? MI : (64 / (CT * 4) > 0 ? 64 / (CT * 4) : 1);
+  auto run = [&](auto FULLC) {
+    constexpr bool FULL = decltype(FULLC)::value;
+    static_for<0, (MI + RCH - 1) / RCH>([&](auto C) {
+      constexpr int i0 = decltype(C)::value * RCH;
+      constexpr int i1 = i0 + RCH < MI ? i0 + RCH : MI;
+      float res[RCH][CT][4];
+      if (add) {
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+#pragma unroll
+          for (int q = 0; q < CT; ++q) {
+            const int n = FULL ? (nt0 + wc + q) * 16 + lm : min((nt0 + wc + q) * 16 + lm, p.N - 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int m = FULL ? m0 + wr + i * 16 + lk * 4 + e : min(m0 + wr + i * 16 + lk * 4 + e, p.M - 1);
+              res[i - i0][q][e] = to_f(out[(long long)m * p.ldo + n]);
+            }
+          }
+      }
+      static_for<i0 * CT, i1 * CT>([&](auto I) {
+        constexpr int i = decltype(I)::value / CT, qd = decltype(I)::value % CT;
+        const f32x4_t a = acc[i][qd];
+        const int nt = nt0 + wc + qd;
+        const int mb = m0 + wr + i * 16 + lk * 4;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (EPI == PF2_GENERIC) {
+            float x = a[e] * rsc[i][e] + cb[qd];
+            if (p.act != QT_ACT_NONE) x = act_f(x, p.act);
+            v[e] = x * cc[qd];
+          } else {
+            v[e] = a[e] * rsc[i][e];
+          }
+        }
+        if (swiglu) {
+          // lanes lm < 8 hold the gate columns, lm >= 8 the matching up columns: every lane forms the products
+          // of column lm & 7 and stores two of the four rows (no idle half)
+          float r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = half_partner<16>(v[e]);
+            const float g = lm < 8 ? v[e] : pv, u = lm < 8 ? pv : v[e];
+            r[e] = silu_fast(g) * u;
+          }
+          const int c = nt * 8 + (lm & 7);
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const int m = mb + (lm < 8 ? e2 : e2 + 2);
+            const float val = lm < 8 ? r[e2] : r[e2 + 2];
+            if (FULL || (m < p.M && nt < ntl && c < (p.N >> 1))) out[(long long)m * p.ldo + c] = from_f<OT>(val);
+          }
+        } else {
+          const int n = nt * 16 + lm;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = mb + e;
+            const float r = add ? res[i - i0][qd][e] + v[e] : v[e];
+            if (FULL || (m < p.M && nt < ntl && n < p.N)) {
+              out[(long long)m * p.ldo + n] = from_f<OT>(r);
+              if constexpr (EPI == PF2_ADD_OUT2) p.out2[(long long)m * p.ldo2 + n] = f2bf(r);
+              else if constexpr (EPI == PF2_GENERIC) { if (p.out2) p.out2[(long long)m * p.ldo2 + n] = f2bf(r); }
+            }
+          }
+        }
+      });
+    });
+  };
+  if (m0 + BM <= p.M && (nt0 + NTB) * 16 <= p.N) run(std::true_type{});
+  else run(std::false_type{});
+  PF2_STAMP(2);
+}
+
+template <typename OT, int BM, int NTB, int NS, int WM = 2, int WN = 2, bool AFL = true>
+void launch_pf2(const GemmP& p, hipStream_t s) {
+  const int ntl = (p.N + 15) / 16;
+  const int nwg = ((p.M + BM - 1) / BM) * ((ntl + NTB - 1) / NTB);
+  const dim3 g(nwg), b(WM * WN * 64);
+  const bool plain = p.act == QT_ACT_NONE && p.bias == nullptr && p.colscale == nullptr;
+  if constexpr (std::is_same<OT, bf16_t>::value) {
+    if (plain && p.epi == QT_EPI_SWIGLU) { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU>), g, b, 0, s, p); return; }
+  } else {
+    if (plain && p.epi == QT_EPI_STORE && !p.out2)
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE>), g, b, 0, s, p); return; }
+    if (plain && p.epi == QT_EPI_ADD && !p.out2)
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD>), g, b, 0, s, p); return; }
+    if (plain && p.epi == QT_EPI_ADD && p.out2)
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2>), g, b, 0, s, p); return; }
+  }
+  hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC>), g, b, 0, s, p);
+}
+
+#ifndef QT_PF2_PROBE
+// Tile configuration (QT_PF2_CFG = 3 / 4 / 9 / 11 forces one, measurement; 0 = chosen by shape).
+// tools/pf2_probe.hip timed every configuration on the 1.7B / 0.6B talker prefill shapes at M = 256 ... 4096
+// (profiles/r03_pf2_probe_sweep.txt): a block's time is nearly independent of M and N (its loop runs K / 64 stages of a
+// fixed tile), so launch time ~ ceil(blocks / resident slots) x block time, and the best tile is the one whose
+// block count quantises best onto the 256 CUs.  Block cycles per 2048 of K and epilogue cycles below are those
+// measurements; cfg 3 (72 KiB of LDS) runs 2 blocks per CU, the others 1.
+struct Pf2Cfg { int id, BM, BN, bpc; float loop1, loop2, epi; };
+constexpr Pf2Cfg PF2_CFGS[] = {
+    {3, 128, 64, 2, 31000.f, 44000.f, 4000.f},   // 4 waves, wave tile 64 x 32
+    {11, 64, 96, 1, 28000.f, 28000.f, 3000.f},   // 4 waves, wave tile 32 x 48
+    {4, 256, 128, 1, 68000.f, 68000.f, 8000.f},  // 8 waves, wave tile 64 x 64
+    {9, 256, 160, 1, 95000.f, 95000.f, 10000.f}, // 4 waves, wave tile 128 x 80
+};
+inline int pf2_cfg_env() {
+  static const int v = [] { const char* e = getenv("QT_PF2_CFG"); return e ? atoi(e) : 0; }();
+  return v;
+}
+inline int pf2_pick(int M, int N, int K) {
+  int best = 3;
+  float best_t = 3.4e38f;
+  for (const Pf2Cfg& c : PF2_CFGS) {
+    const long long blocks = (long long)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
+    const float kf = K / 2048.f;
+    float t;
+    if (c.bpc == 2 && blocks > 256) t = (float)((blocks + 511) / 512) * (c.loop2 * kf + c.epi);
+    else t = (float)((blocks + 255) / 256) * (c.loop1 * kf + c.epi);
+    if (t < best_t) { best_t = t; best = c.id; }
+  }
+  return best;
+}
+
+template <typename OT>
+void launch_pf2_auto(const GemmP& p, hipStream_t s) {
+  int cfg = pf2_cfg_env();
+  if (cfg == 0) cfg = pf2_pick(p.M, p.N, p.Klog);
+  if (cfg == 4) launch_pf2<OT, 256, 8, 3, 4, 2>(p, s);
+  else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);
+  else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);
+  else launch_pf2<OT, 128, 4, 3>(p, s);
+}
+#endif  // QT_PF2_PROBE
+
+}  // namespace
+
+#ifndef QT_PF2_PROBE
+namespace qt_gemm_impl {
+void launch_pf2_auto_f32(const GemmP& p, hipStream_t s) { launch_pf2_auto<float>(p, s); }
+void launch_pf2_auto_bf16(const GemmP& p, hipStream_t s) { launch_pf2_auto<bf16_t>(p, s); }
+}  // namespace qt_gemm_impl
+#endif  // QT_PF2_PROBE

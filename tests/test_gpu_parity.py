@@ -224,15 +224,18 @@ def test_igemm_linear_rms_swiglu_bf16(M, H, I):
     torch.testing.assert_close(xr.cpu(), x + _bf(hb.cpu().float()) @ _bf(down).T, atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("M,N,K,mode", [(2900, 3072, 512, "swiglu"), (2900, 3072, 512, "rms"), (520, 8192, 1024, "rms"),
-                                        (520, 8192, 1024, "add"), (300, 1000, 640, "add"), (300, 1008, 640, "swiglu"),
-                                        (131, 2048, 6144, "add"), (1100, 4096, 512, "rms"), (1300, 2048, 1024, "add")])
+@pytest.mark.parametrize("M,N,K,mode", [
+    (2900, 3072, 512, "swiglu"), (2900, 3072, 512, "rms"), (650, 11856, 512, "swiglu"),   # 256 x 160, 4 waves
+    (520, 8192, 1024, "rms"), (520, 8192, 1024, "add"), (1100, 4096, 512, "rms"),          # 256 x 128, 8 waves
+    (300, 1000, 640, "add"), (300, 1008, 640, "swiglu"), (131, 2048, 6144, "add_plain"),   # 64 x 96, 4 waves
+    (680, 2048, 2048, "add_noshadow"),
+    (1300, 2048, 1024, "add"), (1300, 2048, 1024, "add_plain"), (1300, 2056, 1024, "add_noshadow")])  # 128 x 64
 def test_prefill_gemm_pf2_bf16(M, N, K, mode):
     """Deep-pipelined prefill GEMM (gemm_pf2_k: LDS-DMA operands, NS stages in flight) on bf16 A, every tile
-    configuration the shape rule picks (256 x 128 / 8 waves, 128 x 128 / 8 waves, 128 x 64 / 4 waves), ragged rows /
-    columns:
-    RMSNorm rows from the bf16 A values, SwiGLU epilogue, residual add with the bf16 shadow (out2), vs torch fp32 on
-    the same bf16-rounded operands."""
+    configuration the shape rule picks (256 x 160 / 4 waves, 256 x 128 / 8 waves, 64 x 96 / 4 waves, 128 x 64 /
+    4 waves; comments above), interior and ragged row / column tiles, every epilogue form: RMSNorm rows from the bf16
+    A values (plain store), SwiGLU, residual add with bias (generic form), without bias with / without the bf16
+    shadow (out2) -- vs torch fp32 on the same bf16-rounded operands."""
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
     g = torch.Generator().manual_seed(M + N + K)
@@ -258,15 +261,16 @@ def test_prefill_gemm_pf2_bf16(M, N, K, mode):
         ref = (Af @ _bf(W * gamma).T) * rs
         torch.testing.assert_close(out.cpu(), ref, atol=2e-3, rtol=2e-3)
         return
-    b = torch.randn(N, generator=g) * 0.1
-    t = Kn.tile_linear(W.to(dev), torch.bfloat16, b.to(dev))
+    b = torch.randn(N, generator=g) * 0.1 if mode == "add" else None
+    t = Kn.tile_linear(W.to(dev), torch.bfloat16, None if b is None else b.to(dev))
     x0 = torch.randn(M, N, generator=g)
     out = x0.to(dev).clone()
-    o16 = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+    o16 = None if mode == "add_noshadow" else torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
     Kn.gemm(A.to(dev), t, out, M, K, N, epi=_hip.EPI_ADD, out2=o16)
-    ref = x0 + Af @ _bf(W).T + b
+    ref = x0 + Af @ _bf(W).T + (0 if b is None else b)
     torch.testing.assert_close(out.cpu(), ref, atol=2e-3, rtol=2e-3)
-    torch.testing.assert_close(o16.float().cpu(), _bf(out.cpu()), atol=0, rtol=0)
+    if o16 is not None:
+        torch.testing.assert_close(o16.float().cpu(), _bf(out.cpu()), atol=0, rtol=0)
 
 
 @pytest.mark.parametrize("D,hq,hkv,window", [(128, 16, 8, 0), (16, 4, 2, 0), (64, 4, 4, 5)])
