@@ -938,6 +938,12 @@ inline int gemv_mr() {
   return std::max(1, std::min(16, v));
 }
 
+// largest row count served by the skinny GEMM gemm_sk_k (QT_SK=0 disables it: measurement)
+inline int sk_max_m() {
+  static const int v = [] { const char* e = getenv("QT_SK"); return (e && atoi(e) == 0) ? 0 : 64; }();
+  return v;
+}
+
 // smallest row count routed to the LDS-tiled implicit GEMM (QT_IGEMM_MIN_M overrides, measurement)
 inline int igemm_min_m() {
   static const int v = [] { const char* e = getenv("QT_IGEMM_MIN_M"); return e ? atoi(e) : 128; }();
@@ -965,7 +971,7 @@ inline int pf_nmax() {
 template <typename WT, typename AT>
 bool pf_route(const GemmP& p) {
   return sizeof(WT) == 2 && sizeof(AT) == 2 && p.taps == 0 && pf_on() && p.a_index == nullptr && p.gamma == nullptr &&
-         p.N >= 32 && (pf_nmax() == 0 || p.N <= pf_nmax()) && p.M >= std::max(igemm_min_m(), pf_min_m()) && p.mr > 16 && p.Klog % 8 == 0 && p.lda % 8 == 0 && !p.a_elu &&
+         p.N >= 32 && (pf_nmax() == 0 || p.N <= pf_nmax()) && (p.pf_small || p.M >= std::max(igemm_min_m(), pf_min_m())) && p.mr > 16 && p.Klog % 8 == 0 && p.lda % 8 == 0 && !p.a_elu &&
          p.sn_a == nullptr && !p.no_igemm;
 }
 
@@ -980,6 +986,13 @@ template <typename WT, typename AT, typename OT>
 int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
+  if constexpr (sizeof(WT) == 2 && sizeof(AT) == 2) {
+    if (p.sk) {
+      if constexpr (std::is_same<OT, float>::value) qt_gemm_impl::launch_sk_f32(p, s);
+      else qt_gemm_impl::launch_sk_bf16(p, s);
+      return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+    }
+  }
   if (p.mr <= 16 && p.taps == 0 && p.Klog % KT == 0 && p.gamma == nullptr && !p.a_elu) {
     const int kts = (p.Kp / KT + p.ks - 1) / p.ks;  // k tiles per split
     if (kts >= 48 && p.wpb_max >= 16) launch_gemv<WT, AT, OT, 16>(p, nt, (kts + 15) / 16, s);
@@ -1132,6 +1145,35 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   // talker down 10.9 (split-K 2) -> 9.4, CP down 7.6 -> 6.5, CP lm_head 4.9 -> 4.5 us; wider shapes lose:
   // talker qkv 6.7 -> 9.6).  QT_GEMV_RG = n forces n groups, 1 = off, 0 = auto.
   p.mr = std::max(1, a->M);
+  // 17..256 rows of bf16 A x bf16 weights (prefills of streaming-text / voice-clone prompts, single-request refills):
+  // three kernels, picked by the per-launch times of tools/prefill_gemm_bench.py at 1.7B / 0.6B dims
+  // (profiles/r03_skinny_routes.txt).  The row-group GEMV grows linearly in M (each group re-reads the weights), the
+  // tiled gemm_pf2_k is flat in M but has few blocks on narrow outputs, gemm_sk_k (every row in one block per column
+  // tile) reads the weights once but every block re-reads A:
+  //   outputs >= 4096 columns: gemm_sk_k at <= 48 rows of a <= 8 Mi-element weight (1.7B qkv 24 rows 11.5 -> 7.6 us,
+  //     48 rows 16.5 -> 10.7), else gemm_pf2_k (gate-up 80 rows 51.4 -> 16.2, 112 rows 87.6 -> 16.9; qkv 112 rows
+  //     35.1 -> 16.0);
+  //   narrower outputs: the row-group GEMV while M x N <= 128 x 2048 (o 80 rows 12.2 vs 14.5 on gemm_pf2_k, down
+  //     29.0 vs 35.7), else gemm_pf2_k (o 200 rows 24.3 -> 14.6, down 64.2 -> 35.9).
+  // QT_SKINNY=0 restores the round-2 rule (row-group GEMV up to 96 rows / 256 rows of <= 2048 columns).
+  p.sk = 0;
+  p.pf_small = 0;
+  static const int skinny_env = [] { const char* e = getenv("QT_SKINNY"); return e ? atoi(e) : 1; }();
+  const bool skinny = skinny_env != 0 && a->M > 16 && a->M <= 256 && a->taps == 0 && a->w_dtype == QT_BF16 &&
+                      a->a_dtype == QT_BF16 && a->K % 64 == 0 && a->a_index == nullptr && a->gamma == nullptr &&
+                      a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr && a->lda % 8 == 0 &&
+                      ((size_t)a->A & 15) == 0 && a->N >= 32;
+  bool skinny_gemv = false;
+  if (skinny) {
+    if (a->N >= 4096) {
+      if (a->M <= 48 && (long long)a->N * a->K <= (8ll << 20) && sk_max_m() >= a->M) p.sk = 1;
+      else p.pf_small = 1;
+    } else if ((long long)a->M * a->N <= 128ll * 2048) {
+      skinny_gemv = true;
+    } else {
+      p.pf_small = 1;
+    }
+  }
   static const int rg_env = [] { const char* e = getenv("QT_GEMV_RG"); return e ? atoi(e) : 0; }();
   if (a->M <= 16 && a->taps == 0 && a->w_dtype == QT_BF16 && a->K % KT == 0 && a->gamma == nullptr) {
     // four groups of 2 rows for <= 64 tiles (CP down 6.5 -> 5.8 us; 128-tile shapes lose with four)
@@ -1143,8 +1185,10 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
       // CP down 5.8 -> 5.6 us (o_proj / lm_head keep 16)
       if (wpb_env <= 0 && ktl >= 96) p.wpb_max = 8;
     }
-  } else if (a->M <= gemv_max_m() && (a->M <= 96 || a->N <= 2048) && a->taps == 0 && a->w_dtype == QT_BF16 &&
-             a->K % KT == 0 && a->gamma == nullptr && a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr) {
+  } else if (skinny ? skinny_gemv
+                     : (a->M <= gemv_max_m() && (a->M <= 96 || a->N <= 2048) && a->taps == 0 && a->w_dtype == QT_BF16 &&
+                        a->K % KT == 0 && a->gamma == nullptr && a->a_act == QT_AACT_NONE &&
+                        a->snake_alpha == nullptr)) {
     // skinny GEMM (17..96 rows, or up to gemv_max_m rows of a <= 2048-column output: the talker prefill of
     // streaming-text prompts, short codec windows): the decode GEMV over row groups of 16 -- one block per (column
     // tile, row group), the weight tile streamed from HBM once and re-read from L2 by the other row groups of its
@@ -1159,7 +1203,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   // out2 is written by the decode GEMV's epilogue (M <= 16, or the skinny row-group path above) and by gemm_pf_k
   // (bf16-A prefill linears)
   const bool pf = w == QT_BF16 && a->a_dtype == QT_BF16 && pf_route<bf16_t, bf16_t>(p);
-  if (p.out2 && !pf && (p.mr > 16 || a->K % KT != 0 || a->gamma != nullptr || a->a_act != QT_AACT_NONE))
+  if (p.out2 && !pf && !p.sk && (p.mr > 16 || a->K % KT != 0 || a->gamma != nullptr || a->a_act != QT_AACT_NONE))
     return QT_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int ad = a->a_dtype;

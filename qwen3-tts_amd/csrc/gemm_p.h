@@ -24,10 +24,15 @@ struct GemmP {
   int a_elu;                    // ELU on A (tokenizer encoder convs)
   int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))
   bf16_t* out2; long long ldo2; // optional bf16 copy of the stored output (decode residual stream shadow)
+  int sk;                       // 1: skinny GEMM (gemm_sk_k, 17..64 rows, every row in one block)
+  int pf_small;                 // 1: gemm_pf2_k below its default row floor (17..256-row routing in qt_gemm)
 };
 
 // gemm_pf2_k (gemm_pf2.hip): prefill linears with bf16 A and bf16 pre-tiled W, K % 64 == 0, 16-byte aligned A
 void launch_pf2_auto_f32(const GemmP& p, hipStream_t s);
 void launch_pf2_auto_bf16(const GemmP& p, hipStream_t s);
+// gemm_sk_k (gemm_sk.hip): 17..64 rows, bf16 A and bf16 pre-tiled W, K % 32 == 0, 16-byte aligned A rows
+void launch_sk_f32(const GemmP& p, hipStream_t s);
+void launch_sk_bf16(const GemmP& p, hipStream_t s);
 
 }  // namespace qt_gemm_impl

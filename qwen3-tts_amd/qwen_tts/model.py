@@ -294,6 +294,12 @@ class TTSModel:
         dec = self.speech_tokenizer.model
         up = dec.total_upsample
         RC, RX = self.REF_CHUNK, self.REF_CTX
+        refs = voice_clone_prompt.get("ref_code") if voice_clone_prompt is not None else None
+        prefix = None if refs is None or all(r is None for r in refs) else list(refs)
+        # voice clone: the reference frames every row starts with are known at submit -- their codec decode starts on
+        # a side stream before the (host-bound) prompt assembly, so it runs beside it instead of beside the prefill
+        started = self._start_ref_decode(dec, prefix, len(prefix)) if prefix is not None and left_context is None \
+            else None
         emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
                                                    voice_clone_prompt, ref_ids)
         gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
@@ -307,11 +313,9 @@ class TTSModel:
         cum = [0] * B                     # samples emitted per row
         # chunk sizes double from first_chunk_frames up to chunk_frames: each chunk's audio (80 ms per frame) covers
         # the generation of the next one (~3 ms per frame), so playback started at the first packet never starves
-        refs = voice_clone_prompt.get("ref_code") if voice_clone_prompt is not None else None
-        prefix = None if refs is None or all(r is None for r in refs) else list(refs)
         if left_context is None:
             yield from self._stream_stateful(dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames,
-                                             use_graph, prefix)
+                                             use_graph, prefix, started)
             return
         if prefix is not None:
             raise NotImplementedError("stream(left_context=...) with voice-clone reference codes (ICL): use the "
@@ -390,8 +394,25 @@ class TTSModel:
                 cc[b, g0 + R[b] - lo:g1 + R[b] - lo] = codes[b, g0:g1]
         return cc
 
+    def _start_ref_decode(self, dec, prefix, B):
+        """Feed every row's leading reference frames (the first min(R_b, 300) of them) to a fresh incremental decoder
+        on a side stream; returns (pre, side stream, decoder, frames fed) for _stream_stateful, or None when some row
+        has no reference frames."""
+        dev = self.device
+        pre = [None if x is None else torch.as_tensor(x).to(dev, torch.int32) for x in prefix]
+        if any(x is None or x.shape[0] == 0 for x in pre):
+            return None
+        main = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # (the stream's state slot brings its own split-K workspace)
+            cs = dec.stream(B, self.REF_CTX + self.REF_CHUNK)
+            fed = min(min(int(x.shape[0]) for x in pre), self.REF_CHUNK)
+            cs.feed(torch.stack([x[:fed] for x in pre]))
+        return pre, side, cs, fed
+
     def _stream_stateful(self, dec, emb, mask, trail, pad, gp, B, eos, first_chunk_frames, chunk_frames, use_graph,
-                         prefix=None):
+                         prefix=None, started=None):
         """stream() on the incremental codec: every final frame is fed once to the decoder of its reference chunk
         and every sample computable from the frames fed so far is emitted -- 1920 n - 555 samples of a chunk after
         its n frames, i.e. no lookahead frame is waited for (the 555 samples that need it follow with the next
@@ -408,8 +429,11 @@ class TTSModel:
         up = dec.total_upsample
         RC, RX = self.REF_CHUNK, self.REF_CTX
         dev = self.device
-        pre = [None] * B if prefix is None else [None if x is None else torch.as_tensor(x).to(dev, torch.int32)
-                                                  for x in prefix]
+        if started is not None:
+            pre = started[0]
+        else:
+            pre = [None] * B if prefix is None else [None if x is None else torch.as_tensor(x).to(dev, torch.int32)
+                                                      for x in prefix]
         R = [0 if x is None else int(x.shape[0]) for x in pre]
         pre_nz = [0 if x is None else int((x[:, 0] != 0).sum()) for x in pre]
         end = [None] * B                  # generated frame count of each row once its EOS is seen
@@ -420,15 +444,12 @@ class TTSModel:
         scanned = 0                       # cb0 columns already searched for EOS
         k, cs, fed, emit_s, ctx_s = 0, None, 0, 0, 0   # reference chunk, its decoder, positions fed, samples emitted
         main, side = torch.cuda.current_stream(dev), None
-        if min(R) > 0:
+        if started is not None:  # stream() began decoding the reference frames before the prompt assembly
+            _, side, cs, fed = started
+        elif min(R) > 0:
             # every row starts with reference frames, known at submit: decode them on a side stream while the talker
             # prefills and generates the first frames on this one
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):  # (the stream's state slot brings its own split-K workspace)
-                cs = dec.stream(B, RX + RC)
-                fed = min(min(R), RC)
-                cs.feed(torch.stack([x[:fed] for x in pre]))
+            _, side, cs, fed = self._start_ref_decode(dec, pre, B)
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
                                      first=first_chunk_frames, grow=True)
         try:

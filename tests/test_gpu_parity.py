@@ -273,6 +273,67 @@ def test_prefill_gemm_pf2_bf16(M, N, K, mode):
         torch.testing.assert_close(o16.float().cpu(), _bf(out.cpu()), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("M", [17, 40, 80, 131, 200, 256])
+@pytest.mark.parametrize("N,K,mode", [(2048, 2048, "add"), (1000, 640, "add_noshadow"), (4096, 512, "swiglu"),
+                                      (4096, 1024, "rms"), (1024, 3072, "add_plain"), (12288, 512, "swiglu")])
+def test_skinny_gemm_bf16(M, N, K, mode):
+    """17..256-row GEMMs on bf16 A through qt_gemm's skinny routing (gemm_sk_k: every row in one block per 16-column
+    tile, waves split K; the row-group GEMV; gemm_pf2_k below its old row floor): RMSNorm rows, SwiGLU, residual add
+    with bias / without, with / without the bf16 shadow, ragged row fragments and columns -- vs torch fp32 on the same
+    bf16-rounded operands; on gemm_sk_k and the row-group GEMV every row's bits are independent of M (a request
+    prefilled alone == inside a batch)."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    Af = A.float()
+    rs = torch.rsqrt(Af.pow(2).mean(-1, keepdim=True) + 1e-6)
+    Ad = A.to(dev)
+    if mode == "swiglu":
+        I = N // 2
+        gate, up = torch.randn(I, K, generator=g) * 0.05, torch.randn(I, K, generator=g) * 0.05
+        gamma = 1 + 0.1 * torch.randn(K, generator=g)
+        t = Kn.tile_swiglu(gate.to(dev), up.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+        run = lambda m: Kn.gemm(Ad, t, outs[m], abs(m), K, I, rms=True, eps=1e-6, epi=_hip.EPI_SWIGLU)  # noqa: E731
+        outs = {m: torch.zeros(abs(m), I, device=dev, dtype=torch.bfloat16) for m in (M, -17)}
+        ref = torch.nn.functional.silu((Af @ _bf(gate * gamma).T) * rs) * ((Af @ _bf(up * gamma).T) * rs)
+        tol = 1e-2
+    elif mode == "rms":
+        W = torch.randn(N, K, generator=g) * 0.05
+        gamma = 1 + 0.1 * torch.randn(K, generator=g)
+        t = Kn.tile_linear(W.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+        outs = {m: torch.zeros(abs(m), N, device=dev) for m in (M, -17)}
+        run = lambda m: Kn.gemm(Ad, t, outs[m], abs(m), K, N, rms=True, eps=1e-6)  # noqa: E731
+        ref = (Af @ _bf(W * gamma).T) * rs
+        tol = 2e-3
+    else:
+        W = torch.randn(N, K, generator=g) * 0.05
+        b = torch.randn(N, generator=g) * 0.1 if mode == "add" else None
+        t = Kn.tile_linear(W.to(dev), torch.bfloat16, None if b is None else b.to(dev))
+        x0 = torch.randn(M, N, generator=g)
+        outs = {m: x0[:abs(m)].to(dev).clone() for m in (M, -17)}
+        o16 = {m: (None if mode == "add_noshadow" else torch.zeros(abs(m), N, device=dev, dtype=torch.bfloat16))
+               for m in (M, -17)}
+        run = lambda m: Kn.gemm(Ad, t, outs[m], abs(m), K, N, epi=_hip.EPI_ADD, out2=o16[m])  # noqa: E731
+        ref = x0 + Af @ _bf(W).T + (0 if b is None else b)
+        tol = 2e-3
+    run(M)
+    run(-17)  # the first 17 rows alone (key -17)
+    got = outs[M].float().cpu()
+    torch.testing.assert_close(got, ref, atol=tol, rtol=tol)
+    # qt_gemm's 17..256-row rule (gemm.hip): gemm_sk_k / row-group GEMV rows do not depend on M
+    nw = N
+
+    def route(m):
+        if nw >= 4096:
+            return "sk" if m <= 48 and nw * K <= (8 << 20) else "pf2"
+        return "gemv" if m * nw <= 128 * 2048 else "pf2"
+    if route(M) == route(17) != "pf2":
+        assert torch.equal(outs[-17].float().cpu(), got[:17]), "row results depend on M"
+    if mode in ("add", "add_plain"):
+        torch.testing.assert_close(o16[M].float().cpu(), _bf(outs[M].cpu()), atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("D,hq,hkv,window", [(128, 16, 8, 0), (16, 4, 2, 0), (64, 4, 4, 5)])
 def test_qkv_post_and_attention(D, hq, hkv, window):
     from qwen_tts import kernels as Kn
@@ -318,7 +379,7 @@ def test_qkv_post_and_attention(D, hq, hkv, window):
     torch.testing.assert_close(att.cpu(), ref, atol=2e-5, rtol=2e-5)
 
 
-@pytest.mark.parametrize("D,hq,hkv,L", [(128, 16, 8, 300), (128, 16, 8, 17), (16, 4, 2, 9)])
+@pytest.mark.parametrize("D,hq,hkv,L", [(128, 16, 8, 300), (128, 16, 8, 129), (128, 16, 8, 520), (128, 16, 8, 17), (16, 4, 2, 9)])
 @pytest.mark.parametrize("kvdt", [torch.float32, torch.bfloat16])
 def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
     """Fused qt_decode_attention == qt_qkv_post + qt_attention on the same cache (decode rows)."""

@@ -14,6 +14,8 @@ def main():
     dev = torch.device("cuda:0")
     from qwen_tts import Qwen3TTSModel
     B = int(os.environ.get("QT_FPG_B", "8"))
+    if os.environ.get("QT_FPG_VC"):  # configs[4]: voice-clone prompt (encode + x-vector) + stream first packet
+        return _profile(*_vc_first(B))
     cfg, W, CW = bench.make_weights("1.7b-customvoice", dev, 1, 0)
     tts = Qwen3TTSModel.from_pretrained("synthetic:1.7b-customvoice", device_map=str(dev), dtype=torch.bfloat16,
                                         weights=W, codec_weights=CW)
@@ -29,6 +31,34 @@ def main():
         for _ in m.stream(**kw, **gen):
             break
         torch.cuda.synchronize()
+    _profile(first, B)
+
+
+def _vc_first(B):
+    """configs[4] per GPU (tools/config_bench.py config4): B 3 s reference clips, ICL prompts, 120-token texts."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden"))
+    from cases import ref_audio, ref_text_ids
+    from qwen_tts import Qwen3TTSModel
+    tts = Qwen3TTSModel.from_pretrained("synthetic:1.7b-base", dtype=torch.bfloat16)
+    m = tts.model
+    clips = [(ref_audio(72000, 100 + i), 24000) for i in range(B)]
+    ids = [bench.synth_ids(120, 50 + i) for i in range(B)]
+    ref_ids = [ref_text_ids(40, 60 + i) for i in range(B)]
+    gen = dict(max_new_tokens=257, do_sample=True, top_k=50, top_p=1.0, temperature=0.9, subtalker_dosample=True,
+               subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9, repetition_penalty=1.05,
+               ignore_eos=True)
+
+    def first():
+        items = tts.create_voice_clone_prompt(ref_audio=clips, ref_text=["ref"] * B)
+        vcp = tts._prompt_items_to_voice_clone_prompt(items)
+        for _ in m.stream(input_ids=ids, ref_ids=ref_ids, voice_clone_prompt=vcp, languages=["english"] * B,
+                          non_streaming_mode=False, **gen):
+            break
+        torch.cuda.synchronize()
+    return first, B
+
+
+def _profile(first, B):
     for _ in range(4):
         first()
     from torch.profiler import profile, ProfilerActivity
@@ -42,6 +72,12 @@ def main():
     t_begin = min(e.time_range.start for e in cpu)
     print(f"B={B} wall {wall:.2f} ms; {len(ev)} GPU ops, first at +{(ev[0].time_range.start - t_begin) / 1e3:.2f} ms, "
           f"last ends +{(max(e.time_range.end for e in ev) - t_begin) / 1e3:.2f} ms")
+    dump = os.environ.get("QT_FPG_DUMP")
+    if dump:  # every GPU op: name, stream, start / end in us from the call's start
+        with open(dump, "w") as f:
+            for e in ev:
+                f.write(f"{(e.time_range.start - t_begin) / 1e3:.3f}\t{(e.time_range.end - t_begin) / 1e3:.3f}\t"
+                        f"{getattr(e, 'device_resource_id', -1)}\t{e.name[:90]}\n")
     busy = sum(e.time_range.end - e.time_range.start for e in ev) / 1e3
     print(f"GPU busy {busy:.2f} ms")
     _top(ev)

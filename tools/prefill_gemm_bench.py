@@ -17,6 +17,9 @@ def main():
     xdt = torch.float32 if os.environ.get("QT_PF", "1") == "0" else torch.bfloat16
     shapes = [("qkv", 4096, 2048, True, 0, xdt), ("o", 2048, 2048, False, 1, torch.bfloat16),
               ("gate-up", 12288, 2048, True, 2, xdt), ("down", 2048, 6144, False, 1, torch.bfloat16)]
+    if os.environ.get("QT_PB_DIMS") == "0.6b":  # 0.6B talker / 1.7B code predictor (hidden 1024)
+        shapes = [("qkv", 4096, 1024, True, 0, xdt), ("o", 1024, 2048, False, 1, torch.bfloat16),
+                  ("gate-up", 6144, 1024, True, 2, xdt), ("down", 1024, 3072, False, 1, torch.bfloat16)]
     for M in [int(m) for m in os.environ.get("QT_PB_M", "24,48,80,112,160,256").split(",")]:
         for name, N, Kk, rms, epi, adt in shapes:
             nmat = max(2, int(600e6 // (N * Kk * 2)))

@@ -23,9 +23,9 @@ def main():
     att = torch.zeros(B, hq * D, device=dev, dtype=torch.bfloat16)
     i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
     rb, zero = i32(range(B)), i32([0] * B)
-    for L in (210, 340, 466):
+    for L in [int(x) for x in os.environ.get("ATTN_L", "138,210,267,340,466").split(",")]:
         pos = i32([L - 1] * B)
-        for ns in (1, 2, 4):
+        for ns in [int(x) for x in os.environ.get("ATTN_NS", "1,2,4").split(",")]:
             ws = torch.zeros(K.decode_attn_ws_bytes(B, hq, hkv, D, ns), dtype=torch.uint8, device=dev) if ns > 1 else None
             it = {"i": 0}
 
