@@ -103,28 +103,56 @@ __global__ __launch_bounds__(256) void rvq_stage_k(const float* __restrict__ x, 
                                                    int cb, int D, int R, int* __restrict__ codes, long long codes_ld,
                                                    RvqWs ws) {
   __shared__ float eT[RVQ_MAXD][RVQ_W + 1];
-  __shared__ float rs[RVQ_RB][RVQ_MAXD];
+  __shared__ __attribute__((aligned(16))) float rs[RVQ_RB][RVQ_MAXD];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int s = blockIdx.x, S = gridDim.x, r0 = blockIdx.y * RVQ_RB;
   const int nr = min(RVQ_RB, R - r0);
+  // staging: every load of the slice and of the rows is issued before the first LDS store (16-byte codeword loads;
+  // one scalar load per row element), so the block waits for one round trip instead of one per loop iteration
   const float* tq = tabT + (size_t)q * D * cb + (size_t)s * RVQ_W;
-  for (int i = tid; i < D * RVQ_W; i += 256) eT[i / RVQ_W][i % RVQ_W] = tq[(size_t)(i / RVQ_W) * cb + (i % RVQ_W)];
+  constexpr int EL = RVQ_MAXD * RVQ_W / 4 / 256, RL = RVQ_RB * RVQ_MAXD / 256;
+  f32x4_t ev[EL];
+#pragma unroll
+  for (int j = 0; j < EL; ++j) {
+    const int i = tid + 256 * j, d = min(i / (RVQ_W / 4), D - 1), c4 = (i % (RVQ_W / 4)) * 4;
+    ev[j] = *(const f32x4_t*)(tq + (size_t)d * cb + c4);
+  }
   const float* src = q == 0 ? x : ws.res;
   const long long lds = q == 0 ? ldx : D;
-  for (int i = tid; i < RVQ_RB * D; i += 256) {
-    const int r = i / D, d = i % D;
-    rs[r][d] = r < nr ? src[(long long)(r0 + r) * lds + d] : 0.f;
+  float rv[RL];
+#pragma unroll
+  for (int j = 0; j < RL; ++j) {
+    const int i = tid + 256 * j, r = i / RVQ_MAXD, d = i % RVQ_MAXD;
+    rv[j] = src[(long long)(r0 + min(r, nr - 1)) * lds + min(d, D - 1)];
+  }
+#pragma unroll
+  for (int j = 0; j < EL; ++j) {
+    const int i = tid + 256 * j, d = i / (RVQ_W / 4), c4 = (i % (RVQ_W / 4)) * 4;
+    if (d < D) { eT[d][c4] = ev[j][0]; eT[d][c4 + 1] = ev[j][1]; eT[d][c4 + 2] = ev[j][2]; eT[d][c4 + 3] = ev[j][3]; }
+  }
+#pragma unroll
+  for (int j = 0; j < RL; ++j) {
+    const int i = tid + 256 * j, r = i / RVQ_MAXD, d = i % RVQ_MAXD;
+    rs[r][d] = (r < nr && d < D) ? rv[j] : 0.f;
   }
   __syncthreads();
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const float e = eT[d][lane];
+  // d in order (the same fp32 sums as one d at a time); the 8 rows' values 4 d at a time (16-byte LDS reads)
+  for (int d = 0; d < D; d += 4) {
+    const float e0 = eT[d][lane], e1 = eT[d + 1][lane], e2 = eT[d + 2][lane], e3 = eT[d + 3][lane];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float t = rs[wv * 8 + k][d] - e;
+      const f32x4_t r4 = *(const f32x4_t*)&rs[wv * 8 + k][d];
+      float t = r4[0] - e0;
+      acc[k] = fmaf(t, t, acc[k]);
+      t = r4[1] - e1;
+      acc[k] = fmaf(t, t, acc[k]);
+      t = r4[2] - e2;
+      acc[k] = fmaf(t, t, acc[k]);
+      t = r4[3] - e3;
       acc[k] = fmaf(t, t, acc[k]);
     }
   }
@@ -199,37 +227,66 @@ __global__ __launch_bounds__(256) void mel_logmag_k(const float* __restrict__ sp
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// time statistics: one thread per (item, channel), loops over time (channel-contiguous => coalesced rows)
+// time statistics (attentive statistics pooling): one block per (item, 64 channels), its TS_W waves split time; per
+// wave an online softmax (max, sum of exp) of the logits, then the weighted mean and variance sums, each merged over
+// the waves through LDS in wave order.  (One thread per channel looping over all T frames ran 116 us per call on 4 x
+// 300 frames x 1536 channels.)
+constexpr int TS_W = 8;
 template <typename T>
-__global__ void time_stats_k(const T* __restrict__ x, long long ldx, const float* __restrict__ lg, long long ldl, int B,
-                             int Tn, int C, float eps, float* __restrict__ mean_out, float* __restrict__ std_out,
-                             long long ld_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
-  if (c >= C) return;
-  const T* xc = x + (long long)b * Tn * ldx + c;
+__global__ __launch_bounds__(TS_W * 64) void time_stats_k(const T* __restrict__ x, long long ldx,
+                                                          const float* __restrict__ lg, long long ldl, int B, int Tn,
+                                                          int C, float eps, float* __restrict__ mean_out,
+                                                          float* __restrict__ std_out, long long ld_out) {
+  __shared__ float pm[TS_W][64], ps[TS_W][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, b = blockIdx.y;
+  const int cc = min(c, C - 1);  // clamped: every lane runs the block's barriers
+  const int per = (Tn + TS_W - 1) / TS_W, t0 = min(Tn, w * per), t1 = min(Tn, t0 + per);
+  const T* xc = x + (long long)b * Tn * ldx + cc;
+  const float* lc = lg ? lg + (long long)b * Tn * ldl + cc : nullptr;
   float mx = 0.f, inv = 1.0f / (float)Tn;
-  const float* lc = lg ? lg + (long long)b * Tn * ldl + c : nullptr;
   if (lc) {
-    mx = -INFINITY;
-    for (int t = 0; t < Tn; ++t) mx = fmaxf(mx, lc[(long long)t * ldl]);
+    float m = -INFINITY, s = 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const float v = lc[(long long)t * ldl];
+      if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
+      else s += expf(v - m);
+    }
+    pm[w][lane] = m; ps[w][lane] = s;
+    __syncthreads();
+    mx = pm[0][lane];
+#pragma unroll
+    for (int j = 1; j < TS_W; ++j) mx = fmaxf(mx, pm[j][lane]);
     float se = 0.f;
-    for (int t = 0; t < Tn; ++t) se += expf(lc[(long long)t * ldl] - mx);
+#pragma unroll
+    for (int j = 0; j < TS_W; ++j) se += pm[j][lane] == -INFINITY ? 0.f : ps[j][lane] * expf(pm[j][lane] - mx);
     inv = 1.0f / se;
+    __syncthreads();
   }
   float mean = 0.f;
-  for (int t = 0; t < Tn; ++t) {
+  for (int t = t0; t < t1; ++t) {
     const float wt = lc ? expf(lc[(long long)t * ldl] - mx) * inv : inv;
     mean = fmaf(wt, to_f(xc[(long long)t * ldx]), mean);
   }
-  mean_out[(long long)b * ld_out + c] = mean;
+  pm[w][lane] = mean;
+  __syncthreads();
+  mean = 0.f;
+#pragma unroll
+  for (int j = 0; j < TS_W; ++j) mean += pm[j][lane];
+  if (w == 0 && c < C) mean_out[(long long)b * ld_out + c] = mean;
   if (!std_out) return;
   float var = 0.f;
-  for (int t = 0; t < Tn; ++t) {
+  for (int t = t0; t < t1; ++t) {
     const float wt = lc ? expf(lc[(long long)t * ldl] - mx) * inv : inv;
     const float d = to_f(xc[(long long)t * ldx]) - mean;
     var = fmaf(wt, d * d, var);
   }
-  std_out[(long long)b * ld_out + c] = sqrtf(fmaxf(var, eps));
+  ps[w][lane] = var;
+  __syncthreads();
+  var = 0.f;
+#pragma unroll
+  for (int j = 0; j < TS_W; ++j) var += ps[j][lane];
+  if (w == 0 && c < C) std_out[(long long)b * ld_out + c] = sqrtf(fmaxf(var, eps));
 }
 
 template <typename T>
@@ -310,7 +367,8 @@ extern "C" long long qt_rvq_encode_ws_bytes(int R, int D, int cb) {
 extern "C" int qt_rvq_encode(const float* x, long long ldx, const float* tab, const float* tabT, int Q, int cb, int D,
                              int R, int* codes, long long codes_ld, void* ws, long long ws_bytes, void* stream) {
   if (!x || !tab || !tabT || !codes || !ws || Q < 0 || R < 0) return QT_ERR_ARG;
-  if (cb <= 0 || cb % RVQ_W || D <= 0 || D > RVQ_MAXD) return QT_ERR_SHAPE;
+  if (cb <= 0 || cb % RVQ_W || D <= 0 || D > RVQ_MAXD || D % 4) return QT_ERR_SHAPE;
+  if (((size_t)tabT & 15) != 0) return QT_ERR_ARG;  // 16-byte codeword loads
   if (Q == 0 || R == 0) return QT_OK;
   if (ws_bytes < qt_rvq_encode_ws_bytes(R, D, cb)) return QT_ERR_ARG;
   const int S = cb / RVQ_W;
@@ -338,10 +396,10 @@ extern "C" int qt_time_stats(const void* x, int dtype, long long ldx, const floa
   const dim3 grid(nblk(C, 64), B);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == QT_F32)
-    hipLaunchKernelGGL(time_stats_k<float>, grid, dim3(64), 0, s, (const float*)x, ldx, logits, ldl, B, T, C, eps,
+    hipLaunchKernelGGL(time_stats_k<float>, grid, dim3(TS_W * 64), 0, s, (const float*)x, ldx, logits, ldl, B, T, C, eps,
                        mean_out, std_out, ld_out);
   else if (dtype == QT_BF16)
-    hipLaunchKernelGGL(time_stats_k<bf16_t>, grid, dim3(64), 0, s, (const bf16_t*)x, ldx, logits, ldl, B, T, C, eps,
+    hipLaunchKernelGGL(time_stats_k<bf16_t>, grid, dim3(TS_W * 64), 0, s, (const bf16_t*)x, ldx, logits, ldl, B, T, C, eps,
                        mean_out, std_out, ld_out);
   else return QT_ERR_DTYPE;
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;

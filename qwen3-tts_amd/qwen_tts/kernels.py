@@ -125,6 +125,19 @@ def gemm_workspace(device):
     return _WS[idx]
 
 
+_SIDE = {}
+
+
+def side_stream(device):
+    """A persistent side stream per device for work overlapped with the current stream (the voice-clone front ends,
+    the reference-frame codec decode).  Persistent so its caching-allocator pool is reused: a fresh stream per call
+    allocates fresh blocks, and hipMalloc stalls the host until the GPU is idle, which serialised the overlap."""
+    idx = torch.device(device).index or 0
+    if idx not in _SIDE:
+        _SIDE[idx] = torch.cuda.Stream(device=device)
+    return _SIDE[idx]
+
+
 class use_workspace:
     """`with use_workspace(ws):` routes decode-GEMV split-K through `ws` (e.g. one per row-group stream)."""
 

@@ -10,6 +10,7 @@ from typing import Dict, List, Optional
 
 import torch
 
+from . import kernels as K
 from .talker import GenParams, TalkerEngine
 
 
@@ -403,7 +404,7 @@ class TTSModel:
         if any(x is None or x.shape[0] == 0 for x in pre):
             return None
         main = torch.cuda.current_stream(dev)
-        side = torch.cuda.Stream(device=dev)
+        side = K.side_stream(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):  # (the stream's state slot brings its own split-K workspace)
             cs = dec.stream(B, self.REF_CTX + self.REF_CHUNK)
