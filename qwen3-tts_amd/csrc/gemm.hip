@@ -1116,7 +1116,13 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   const long long wbytes = (long long)((a->N + 15) / 16) * 16 * p.Kp * (a->w_dtype == QT_BF16 ? 2 : 4);
   p.ntl = nt_env >= 0 ? nt_env : (wbytes >= (16ll << 20));
   // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
-  p.ks = 1; p.cnt = nullptr; p.part = nullptr;
+  p.ks = 1; p.cnt = nullptr; p.part = nullptr; p.part_bytes = 0;
+  if (a->M > 16 && a->ws && a->ws_bytes >= QT_GEMM_WS_MIN && a->splitk != 1) {
+    // gemm_pf2_k split-K records (narrow outputs with few tiles, gemm_pf2.hip pf2_splits)
+    p.cnt = (unsigned*)a->ws;
+    p.part = (float*)((char*)a->ws + 4096 * sizeof(unsigned));
+    p.part_bytes = a->ws_bytes - 4096 * (long long)sizeof(unsigned);
+  }
   // wide grids use smaller blocks so several fit per CU (fewer block rounds; measured: N=12288 K=2048
   // 14.7 us at 16 waves/block -> 12.0 at 4); QT_GEMV_WPB overrides the cap for A/B measurement
   static const int wpb_env = [] { const char* e = getenv("QT_GEMV_WPB"); return e ? atoi(e) : 0; }();
@@ -1153,8 +1159,10 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   //   outputs >= 4096 columns: gemm_sk_k at <= 48 rows of a <= 8 Mi-element weight (1.7B qkv 24 rows 11.5 -> 7.6 us,
   //     48 rows 16.5 -> 10.7), else gemm_pf2_k (gate-up 80 rows 51.4 -> 16.2, 112 rows 87.6 -> 16.9; qkv 112 rows
   //     35.1 -> 16.0);
-  //   narrower outputs: the row-group GEMV while M x N <= 128 x 2048 (o 80 rows 12.2 vs 14.5 on gemm_pf2_k, down
-  //     29.0 vs 35.7), else gemm_pf2_k (o 200 rows 24.3 -> 14.6, down 64.2 -> 35.9).
+  //   narrower outputs: the row-group GEMV while M x N x K <= 400 Mi (1.7B o up to 100 rows: 80 rows 12.2 vs 13.0 us
+  //     on gemm_pf2_k; 1.7B down up to 33 rows: 24 rows 11.5 vs 16.9), else gemm_pf2_k with its narrow-output
+  //     split-K (1.7B down 80 rows 29.0 -> 16.9, 112 rows 37.7 -> 17.7; o 112 rows 15.5 -> 13.8, 200 rows 24.3 -> 13.5;
+  //     profiles/r03_skinny_routes.txt).
   // QT_SKINNY=0 restores the round-2 rule (row-group GEMV up to 96 rows / 256 rows of <= 2048 columns).
   p.sk = 0;
   p.pf_small = 0;
@@ -1168,7 +1176,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
     if (a->N >= 4096) {
       if (a->M <= 48 && (long long)a->N * a->K <= (8ll << 20) && sk_max_m() >= a->M) p.sk = 1;
       else p.pf_small = 1;
-    } else if ((long long)a->M * a->N <= 128ll * 2048) {
+    } else if ((long long)a->M * a->N * a->K <= (400ll << 20)) {
       skinny_gemv = true;
     } else {
       p.pf_small = 1;

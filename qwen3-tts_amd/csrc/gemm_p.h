@@ -19,7 +19,8 @@ struct GemmP {
   int wpb_max;                  // waves-per-block cap of the decode GEMV (16, or 8 for wide grids)
   int no_igemm;                 // 1: keep large-M GEMMs on gemm_wt (A/B measurement)
   int ntl;                      // 1: non-temporal weight loads (decode GEMV over >= 16 MiB of weights)
-  unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16]
+  unsigned* cnt; float* part;   // split-K arrival counters [ntiles] + partials [ntiles][ks][64*4+16] (GEMV) /
+  long long part_bytes;         //   gemm_pf2_k split records (17+ rows), part_bytes of room
   const float* sn_a; const float* sn_ib;  // optional SnakeBeta on A (per input channel)
   int a_elu;                    // ELU on A (tokenizer encoder convs)
   int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))

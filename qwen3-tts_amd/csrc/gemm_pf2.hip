@@ -2,6 +2,7 @@
 // codec pre-transformer linears on bf16 activations), routed here by qt_gemm (gemm.hip) for bf16 A + bf16 pre-tiled
 // weights with K % 64 == 0.  Own translation unit so the tile configurations build in parallel with gemm.hip.
 #include "gemm_p.h"
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -20,6 +21,8 @@ namespace {
 using qt_gemm_impl::GemmP;
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+constexpr int PF2_KS_MAX = 4;  // split-K factor bound (narrow outputs)
 
 // SiLU from the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each, 4 instructions): the IEEE
 // division + range-reduced expf of silu_f cost ~40 VALU per element, which made the SwiGLU epilogue of a
@@ -65,7 +68,7 @@ QT_DEV void static_for(F&& f) {
 // ABL (measurement only, tools/pf2_probe.hip), bit mask: 1 no MFMA (fragment reads kept live), 2 no loads after the
 // prologue (the rest runs on stale stages), 4 no fragment reads (and no MFMA), 8 no epilogue (accumulators kept live)
 enum { PF2_GENERIC = -1, PF2_STORE = 0, PF2_ADD = 1, PF2_SWIGLU = 2, PF2_ADD_OUT2 = 3 };
-template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL, int EPI, int ABL = 0>
+template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL, int EPI, int ABL = 0, bool SPLIT = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   constexpr int NW = WM * WN;
   constexpr int MI = BM / WM / 16;            // row fragments per wave
@@ -75,13 +78,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   constexpr int GA = A_FR / NW, GB = B_FR / NW, G = GA + GB;  // DMA instructions per wave per stage
   static_assert(A_FR % NW == 0 && B_FR % NW == 0 && MI >= 1 && CT >= 1, "fragments split over the waves");
   // NS stages, then the row sums of squares: WN partial sums per row (one per wave of a row block)
-  __shared__ __attribute__((aligned(16))) bf16_t smem_pf2[NS * STAGE + 2 * WN * BM];
+  // (one __shared__ object: the split-K arrival flag lives at its end, after the row sums)
+  __shared__ __attribute__((aligned(16))) bf16_t smem_pf2[NS * STAGE + 2 * WN * BM + 8];
   float* ss_row = (float*)(smem_pf2 + NS * STAGE);
   PF2_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lm = lane & 15, lk = lane >> 4;
-  const int ntl = (p.N + 15) / 16, ktiles = p.Kp / 32, S = p.Klog / 64;
+  const int ntl = (p.N + 15) / 16, ktiles = p.Kp / 32, S_all = p.Klog / 64;
+  // split-K (narrow outputs with few tiles): block z of gridDim.y runs stages [s_lo, s_lo + S)
+  // (a separate instantiation: the merge's code after the loop made hipcc keep the accumulators in AGPRs and copy
+  // them through VGPRs every k step of the unsplit kernel, +15-20 %)
+  const int KS = SPLIT ? (int)gridDim.y : 1, z = SPLIT ? (int)blockIdx.y : 0;
+  const int s_lo = S_all * z / KS, S = S_all * (z + 1) / KS - s_lo;
   // XCD-aware tile order: blocks that share an XCD (linear id % 8) take consecutive tiles, row tiles fastest
   const int mtiles = (p.M + BM - 1) / BM, ctiles = (ntl + NTB - 1) / NTB;
   const int nwg = mtiles * ctiles, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
@@ -94,8 +103,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   // this lane's DMA sources: A fragment f = w * GA + i covers rows (f >> 1) * 16.., k tile f & 1
   const int arow = min(m0 + lm, p.M - 1);
   const unsigned lbase = lds_u32(smem_pf2);
-  auto issue = [&](int st) {
-    const unsigned sb = lbase + (unsigned)((st % NS) * STAGE * 2);
+  auto issue = [&](int ls) {  // local stage ls of this split: LDS buffer ls % NS, k offset of global stage s_lo + ls
+    const unsigned sb = lbase + (unsigned)((ls % NS) * STAGE * 2);
+    const int st = s_lo + ls;
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int f = w * GA + i;
@@ -187,6 +197,74 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
       if (lane < 16) ss_row[wj * BM + wr + i * 16 + lane] = v;
     }
     __syncthreads();  // (no DMA in flight any more)
+  }
+  if constexpr (SPLIT) {
+    // deterministic split-K: every split stores its accumulators (and row sums of squares) write-through, one lane
+    // counts the arrival after every storing wave's drain + a barrier, and the last split to arrive sums all splits'
+    // records in split order, then runs the epilogue (MI355X_MICROARCH.md visibility table, first row)
+    constexpr int FR = MI * CT, REC = NW * FR * 256 + WN * BM;  // floats per split record
+    int& pf2_last = *(int*)(smem_pf2 + NS * STAGE + 2 * WN * BM);
+    unsigned long long* rec = (unsigned long long*)(p.part + ((size_t)wg * KS + z) * REC);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        unsigned long long* d = rec + ((w * FR + i * CT + j) * 256 + lane * 4) / 2;
+        __hip_atomic_store(d, __builtin_bit_cast(unsigned long long, (f32x2_t){acc[i][j][0], acc[i][j][1]}),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, __builtin_bit_cast(unsigned long long, (f32x2_t){acc[i][j][2], acc[i][j][3]}),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    float* srec = (float*)rec + NW * FR * 256;
+    if (norm)
+      for (int e = tid; e < WN * BM; e += NW * 64)
+        __hip_atomic_store(srec + e, ss_row[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival is counted
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.cnt + wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pf2_last = old == (unsigned)KS - 1;
+      if (pf2_last) __hip_atomic_store(p.cnt + wg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    __syncthreads();
+    if (!pf2_last) return;
+    const unsigned long long* base = (const unsigned long long*)(p.part + (size_t)wg * KS * REC);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    f32x2_t v[PF2_KS_MAX][MI][CT][2];  // every split's record in flight before the adds
+#pragma unroll
+    for (int zz = 0; zz < PF2_KS_MAX; ++zz)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+          const unsigned long long* d =
+              base + ((size_t)min(zz, KS - 1) * REC + (w * FR + i * CT + j) * 256 + lane * 4) / 2;
+          v[zz][i][j][0] = __builtin_bit_cast(f32x2_t, __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          v[zz][i][j][1] = __builtin_bit_cast(f32x2_t, __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+#pragma unroll
+    for (int zz = 0; zz < PF2_KS_MAX; ++zz)  // split order
+      if (zz < KS) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < CT; ++j) {
+            acc[i][j][0] += v[zz][i][j][0][0]; acc[i][j][1] += v[zz][i][j][0][1];
+            acc[i][j][2] += v[zz][i][j][1][0]; acc[i][j][3] += v[zz][i][j][1][1];
+          }
+      }
+    if (norm) {
+      const float* sb = (const float*)base + NW * FR * 256;
+      for (int e = tid; e < WN * BM; e += NW * 64) {
+        float t = 0.f;
+        for (int zz = 0; zz < KS; ++zz) t += __hip_atomic_load(sb + (size_t)zz * REC + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ss_row[e] = t;
+      }
+      __syncthreads();
+    }
   }
   if constexpr ((ABL & 8) != 0) {
 #pragma unroll
@@ -306,12 +384,44 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   PF2_STAMP(2);
 }
 
+// split-K factor for a launch of nwg tiles: narrow (<= 2048-column) outputs whose tiles leave most CUs idle split K
+// (>= 16 stages of 64 per split; wide outputs measured slower split: 1.7B q/k/v at 80 rows 15.5 -> 17.9 us) when the caller's workspace holds the split records (QT_PF2_SPLIT=0 disables, measurement)
+template <int BM, int NTB, int WM, int WN>
+int pf2_splits(const GemmP& p, int nwg) {
+  static const int env = [] { const char* e = getenv("QT_PF2_SPLIT"); return e ? atoi(e) : 1; }();
+  const int S = p.Klog / 64;
+  if (!env || p.part == nullptr || p.cnt == nullptr || p.N > 2048 || nwg >= 192 || S < 32) return 1;
+  int ks = std::min({PF2_KS_MAX, 256 / nwg, S / 16});
+  constexpr int NW = WM * WN, MI = BM / WM / 16, CT = NTB / WN;
+  const long long rec = (long long)NW * MI * CT * 256 + WN * BM;
+  while (ks > 1 && (long long)nwg * ks * rec * 4 > p.part_bytes) --ks;
+  return std::max(ks, 1);
+}
+
 template <typename OT, int BM, int NTB, int NS, int WM = 2, int WN = 2, bool AFL = true>
 void launch_pf2(const GemmP& p, hipStream_t s) {
   const int ntl = (p.N + 15) / 16;
   const int nwg = ((p.M + BM - 1) / BM) * ((ntl + NTB - 1) / NTB);
-  const dim3 g(nwg), b(WM * WN * 64);
+  const int ks = BM <= 128 ? pf2_splits<BM, NTB, WM, WN>(p, nwg) : 1;
+  const dim3 g(nwg, ks), b(WM * WN * 64);
   const bool plain = p.act == QT_ACT_NONE && p.bias == nullptr && p.colscale == nullptr;
+  if constexpr (BM <= 128) {
+    if (ks > 1) {  // narrow outputs: the split instantiations
+      if constexpr (std::is_same<OT, bf16_t>::value) {
+        if (plain && p.epi == QT_EPI_SWIGLU)
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU, 0, true>), g, b, 0, s, p); return; }
+      } else {
+        if (plain && p.epi == QT_EPI_STORE && !p.out2)
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE, 0, true>), g, b, 0, s, p); return; }
+        if (plain && p.epi == QT_EPI_ADD && !p.out2)
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD, 0, true>), g, b, 0, s, p); return; }
+        if (plain && p.epi == QT_EPI_ADD && p.out2)
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2, 0, true>), g, b, 0, s, p); return; }
+      }
+      hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC, 0, true>), g, b, 0, s, p);
+      return;
+    }
+  }
   if constexpr (std::is_same<OT, bf16_t>::value) {
     if (plain && p.epi == QT_EPI_SWIGLU) { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU>), g, b, 0, s, p); return; }
   } else {

@@ -111,10 +111,13 @@ _WS = {}
 _ACTIVE_WS = []
 
 
+WS_BYTES = 16 << 20  # >= GEMM_WS_MIN: room for gemm_pf2_k's split-K records of the 17+-row linears
+
+
 def new_workspace(device):
-    """Split-K scratch of the decode GEMV (arrival counters must start at zero; every launch re-arms them).
-    One workspace per concurrently running stream."""
-    return torch.zeros(_hip.GEMM_WS_MIN, dtype=torch.uint8, device=device)
+    """Split-K scratch of the decode GEMV and of gemm_pf2_k's narrow-output split-K (arrival counters must start at
+    zero; every launch re-arms them).  One workspace per concurrently running stream."""
+    return torch.zeros(max(WS_BYTES, _hip.GEMM_WS_MIN), dtype=torch.uint8, device=device)
 
 
 def gemm_workspace(device):
@@ -155,7 +158,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
          act=_hip.ACT_NONE, epi=_hip.EPI_STORE, a_index=None, conv=None, use_bias=True, splitk=0, snake=None,
          a_act=_hip.AACT_NONE, out2=None, ldo2=None):
     """conv = (t_in, t_out, t_off, dil) for implicit-conv weights.  splitk: 0 auto, 1 off, n forced
-    (decode GEMV only, needs gemm_workspace(device) allocated).  snake = (alpha, inv_beta): SnakeBeta applied
+    (decode GEMV; 0 / 1 also for gemm_pf2_k's narrow-output split-K; needs gemm_workspace(device) allocated).  snake = (alpha, inv_beta): SnakeBeta applied
     to A per input channel inside the GEMM (fused codec activation).  out2: bf16 copy of the stored fp32 output
     (M <= 16; the decode residual stream's shadow read by the next RMS-normalised GEMV)."""
     a = _hip.GemmArgs()
@@ -174,7 +177,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     if out2 is not None:
         a.out2, a.ldo2 = ptr(out2), ldo if ldo2 is None else ldo2
     ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
-    if ws is not None and M <= 16 and not W.taps:
+    if ws is not None and not W.taps:
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
     if W.taps:
         t_in, t_out, t_off, dil = conv

@@ -273,6 +273,45 @@ def test_prefill_gemm_pf2_bf16(M, N, K, mode):
         torch.testing.assert_close(o16.float().cpu(), _bf(out.cpu()), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(200, 2048, 6144, "add"), (200, 2048, 2048, "add_shadow"),
+                                        (300, 1024, 3072, "rms"), (256, 1000, 2048, "add"), (700, 2048, 6144, "add")])
+def test_prefill_gemm_pf2_splitk(M, N, K, mode):
+    """gemm_pf2_k split-K (narrow outputs whose tiles leave most CUs idle: K split over up to 4 blocks per tile, the
+    last split to arrive sums every split's record in split order): matches the unsplit kernel (splitk=1) to fp32
+    rounding and torch fp32, is bitwise reproducible, keeps the RMS rows / residual / bf16 shadow epilogues."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    Kn.gemm_workspace(dev)
+    g = torch.Generator().manual_seed(M + N + K + 1)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    Af = A.float()
+    W = torch.randn(N, K, generator=g) * 0.05
+    if mode == "rms":
+        gamma = 1 + 0.1 * torch.randn(K, generator=g)
+        t = Kn.tile_linear(W.to(dev), torch.bfloat16, gamma=gamma.to(dev))
+        ref = (Af @ _bf(W * gamma).T) * torch.rsqrt(Af.pow(2).mean(-1, keepdim=True) + 1e-6)
+        outs = []
+        for sk in (0, 0, 1):
+            o = torch.zeros(M, N, device=dev)
+            Kn.gemm(A.to(dev), t, o, M, K, N, rms=True, eps=1e-6, splitk=sk)
+            outs.append((o.cpu(), None))
+    else:
+        t = Kn.tile_linear(W.to(dev), torch.bfloat16)
+        x0 = torch.randn(M, N, generator=g)
+        ref = x0 + Af @ _bf(W).T
+        outs = []
+        for sk in (0, 0, 1):
+            o = x0.to(dev).clone()
+            o16 = torch.zeros(M, N, device=dev, dtype=torch.bfloat16) if mode == "add_shadow" else None
+            Kn.gemm(A.to(dev), t, o, M, K, N, epi=_hip.EPI_ADD, out2=o16, splitk=sk)
+            outs.append((o.cpu(), None if o16 is None else o16.cpu()))
+    torch.testing.assert_close(outs[0][0], ref, atol=2e-3, rtol=2e-3)
+    assert torch.equal(outs[0][0], outs[1][0]), "split-K not reproducible"
+    torch.testing.assert_close(outs[0][0], outs[2][0], atol=2e-5, rtol=2e-5)
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1].float(), _bf(outs[0][0]))
+
+
 @pytest.mark.parametrize("M", [17, 40, 80, 131, 200, 256])
 @pytest.mark.parametrize("N,K,mode", [(2048, 2048, "add"), (1000, 640, "add_noshadow"), (4096, 512, "swiglu"),
                                       (4096, 1024, "rms"), (1024, 3072, "add_plain"), (12288, 512, "swiglu")])
@@ -327,7 +366,7 @@ def test_skinny_gemm_bf16(M, N, K, mode):
     def route(m):
         if nw >= 4096:
             return "sk" if m <= 48 and nw * K <= (8 << 20) else "pf2"
-        return "gemv" if m * nw <= 128 * 2048 else "pf2"
+        return "gemv" if m * nw * K <= (400 << 20) else "pf2"
     if route(M) == route(17) != "pf2":
         assert torch.equal(outs[-17].float().cpu(), got[:17]), "row results depend on M"
     if mode in ("add", "add_plain"):

@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from microbench import timed  # noqa: E402
 
 dev = torch.device("cuda:0")
+K.gemm_workspace(dev)  # the engine passes one (split-K of the decode GEMV and of gemm_pf2_k)
 
 
 def main():
