@@ -944,6 +944,12 @@ inline int sk_max_m() {
   return v;
 }
 
+// largest row count of a conv routed to im2col + the linear GEMMs (QT_IM2COL_MAX_M, measurement)
+inline int im2col_max_m() {
+  static const int v = [] { const char* e = getenv("QT_IM2COL_MAX_M"); return e ? atoi(e) : 256; }();
+  return v;
+}
+
 // smallest row count routed to the LDS-tiled implicit GEMM (QT_IGEMM_MIN_M overrides, measurement)
 inline int igemm_min_m() {
   static const int v = [] { const char* e = getenv("QT_IGEMM_MIN_M"); return e ? atoi(e) : 128; }();
@@ -1080,8 +1086,72 @@ __global__ void tile_weight_k(const T* __restrict__ src, T* __restrict__ dst, in
 
 }  // namespace
 
+namespace {
+// im2col for short conv windows (qt_gemm's small-M conv route below): row m = (item b, output step t), column
+// j * cin_pad + c = input channel c at time t + t_off + j * dil of item b (zero outside [0, t_in) and past cin), with
+// the ELU / SnakeBeta prologue applied and the value rounded to bf16 exactly as igemm_k stages it.  One thread per
+// (row, tap, 8-channel group), 16-byte loads and stores.
+template <typename AT>
+__global__ __launch_bounds__(256) void im2col_k(GemmP p, bf16_t* __restrict__ out) {
+  const int g = p.cin_pad / 8, tg = p.taps * g;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)p.M * tg) return;
+  const int m = (int)(idx / tg), r = (int)(idx % tg), j = r / g, ch = (r % g) * 8;
+  const int b = m / p.t_out, t = m % p.t_out, ti = t + p.t_off + j * p.dil;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  if (ti >= 0 && ti < p.t_in && ch < p.cin) load8f((const AT*)p.A + ((long long)b * p.t_in + ti) * p.lda + ch, v);
+  if (p.a_elu) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = elu_f(v[e]);
+  }
+  if (p.sn_a && ch < p.cin) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sn = __sinf(v[e] * p.sn_a[ch + e]);
+      v[e] = v[e] + p.sn_ib[ch + e] * (sn * sn);
+    }
+  }
+  *(u32x4_t*)(out + (long long)m * p.Kp + j * p.cin_pad + ch) =
+      u32x4_t{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+}
+
+// short conv windows (a streamed codec window's early stages: tens of rows, K = taps x cin_pad up to ~7k): igemm_k's
+// 128-row tiles leave a few dozen blocks each walking hundreds of k chunks (~110-130 us per conv at B = 8 x 1 frame);
+// as im2col + the linear routes (decode GEMV / skinny GEMMs / split-K prefill GEMM) the weights stream over the chip.
+// The im2col image lives in the upper half of the caller's workspace.  QT_IM2COL=0 disables (measurement).
+constexpr long long IM2COL_WS = 16ll << 20, IM2COL_OFF = 8ll << 20;
+inline bool im2col_route(const qt_gemm_args* a) {
+  static const int env = [] { const char* e = getenv("QT_IM2COL"); return e ? atoi(e) : 1; }();
+  if (!env || a->taps <= 0 || a->w_dtype != QT_BF16 || a->M <= 0 || a->M > im2col_max_m() || a->rmsnorm ||
+      a->gamma != nullptr || a->a_index != nullptr || !a->ws || a->ws_bytes < IM2COL_WS || a->t_out <= 0 ||
+      a->cin_pad % 32 || a->cin % 8 || a->splitk == 1)
+    return false;
+  const long long kp = (long long)a->taps * a->cin_pad;
+  return (long long)a->M * kp * 2 <= IM2COL_WS - IM2COL_OFF && a->M % a->t_out == 0;
+}
+}  // namespace
+
 extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   if (!a || !a->A || !a->W || !a->out) return QT_ERR_ARG;
+  if (im2col_route(a)) {
+    GemmP q;
+    q.M = a->M; q.A = a->A; q.lda = a->lda; q.taps = a->taps; q.dil = a->dil > 0 ? a->dil : 1; q.cin = a->cin;
+    q.cin_pad = a->cin_pad; q.t_in = a->t_in; q.t_out = a->t_out; q.t_off = a->t_off; q.Kp = a->taps * a->cin_pad;
+    q.a_elu = a->a_act == QT_AACT_ELU; q.sn_a = a->snake_alpha; q.sn_ib = a->snake_inv_beta;
+    bf16_t* img = (bf16_t*)((char*)a->ws + IM2COL_OFF);
+    const long long n = (long long)a->M * a->taps * (a->cin_pad / 8);
+    hipStream_t s = (hipStream_t)stream;
+    if (a->a_dtype == QT_BF16) hipLaunchKernelGGL(im2col_k<bf16_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, img);
+    else if (a->a_dtype == QT_F32) hipLaunchKernelGGL(im2col_k<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, img);
+    else return QT_ERR_DTYPE;
+    if (hipGetLastError() != hipSuccess) return QT_ERR_LAUNCH;
+    qt_gemm_args b = *a;
+    b.taps = 0; b.A = img; b.a_dtype = QT_BF16; b.lda = q.Kp; b.K = (int)q.Kp; b.a_act = QT_AACT_NONE;
+    b.snake_alpha = nullptr; b.snake_inv_beta = nullptr; b.ws_bytes = IM2COL_OFF;  // split records below the image
+    return qt_gemm(&b, stream);
+  }
   const int E = a->w_dtype == QT_BF16 ? 8 : 4;
   const int KT = 4 * E;
   GemmP p;

@@ -177,7 +177,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     if out2 is not None:
         a.out2, a.ldo2 = ptr(out2), ldo if ldo2 is None else ldo2
     ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
-    if ws is not None and not W.taps:
+    if ws is not None:  # (convs: the short-window im2col route keeps its image in the workspace's upper half)
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
     if W.taps:
         t_in, t_out, t_off, dil = conv

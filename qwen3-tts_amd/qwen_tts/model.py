@@ -11,7 +11,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import kernels as K
-from .talker import GenParams, TalkerEngine
+from .talker import MIN_NEW_TOKENS, GenParams, TalkerEngine
 
 
 class _Runs:
@@ -178,6 +178,8 @@ class TTSModel:
                     pl["trail"] = runs.text(ids[4:-5])
             plans.append(pl)
         runs.run(e)
+        if not any(pl["icl"] for pl in plans):
+            return self._assemble_indexed(runs, plans, h_ins, h_special, non_streaming_mode)
         special = runs.get(h_special)[0]
         bos_e, eos_e, pad_e = special[0].view(1, 1, -1), special[1].view(1, 1, -1), special[2].view(1, 1, -1)
         per: List[list] = [[] if h_ins[i] is None else [runs.get(h_ins[i])] for i in range(B)]
@@ -219,6 +221,63 @@ class TTSModel:
         trail = pad_e.reshape(1, 1, H).expand(B, T, H).clone()
         for i, tr in enumerate(trailing):
             trail[i, :tr.shape[1]] = tr[0]
+        return embeds, mask, trail, pad_e
+
+    def _assemble_indexed(self, runs, plans, h_ins, h_special, non_streaming_mode):
+        """build_prompts' assembly for non-ICL rows as one gather: every prompt / trailing position is the sum of at
+        most two rows of [text projections; codec embeddings; x-vectors; zero row], so the host writes a [positions,
+        2] index table and three GPU ops build the whole batch (the per-row slicing / cat / add chain was ~120
+        host-bound launches at B = 8).  Same two fp32 operands per position as that chain, so the same bits."""
+        B = len(plans)
+        out_t, out_c = runs.out.get("t"), runs.out.get("c")
+        NT = 0 if out_t is None else out_t.shape[0]
+        NC = 0 if out_c is None else out_c.shape[0]
+        vecs = [pl["spk_vec"] for pl in plans if pl["spk_vec"] is not None]
+        Z = NT + NC + len(vecs)  # the zero row
+
+        def t(h, j=0):
+            return h[1] + j
+
+        def c(h, j=0):
+            return NT + h[1] + j
+        sp = h_special
+        bos, eos, pad = t(sp, 0), t(sp, 1), t(sp, 2)
+        seqs, trails, v = [], [], 0
+        for i, pl in enumerate(plans):
+            pos = [] if h_ins[i] is None else [(t(h_ins[i], j), Z) for j in range(h_ins[i][2])]
+            pos += [(t(pl["role"], j), Z) for j in range(3)]
+            ci = [c(pl["c0"], j) for j in range(pl["c0"][2])]
+            if "spk_code" in pl:
+                ci.append(c(pl["spk_code"]))
+            elif pl["spk_vec"] is not None:
+                ci.append(NT + NC + v)
+                v += 1
+            ci += [c(pl["c1"], j) for j in range(2)]
+            pos += [(pad if k < len(ci) - 2 else bos, ci[k]) for k in range(len(ci) - 1)]
+            if non_streaming_mode:
+                n = pl["txt"][2]
+                pos += [(t(pl["txt"], j) if j < n else eos, c(pl["txt_pad"], j)) for j in range(n + 1)]
+                pos.append((pad, c(pl["end_bos"])))
+                trails.append([(pad, Z)])
+            else:
+                if pl["first"][2]:  # (a prompt without a first text token has no such position, as in the chain)
+                    pos.append((t(pl["first"]), ci[-1]))
+                trails.append([(t(pl["trail"], j), Z) for j in range(pl["trail"][2])] + [(eos, Z)])
+            seqs.append(pos)
+        P, T = max(len(s) for s in seqs), max(len(tr) for tr in trails)
+        idx = [[(Z, Z)] * (P - len(s)) + s for s in seqs] + [tr + [(pad, Z)] * (T - len(tr)) for tr in trails]
+        H = (out_t if out_t is not None else out_c).shape[1]
+        parts = [x for x in (out_t, out_c) if x is not None] + [x.reshape(1, H) for x in vecs] + \
+            [torch.zeros(1, H, device=self.device)]
+        table = torch.cat(parts, 0)
+        ix = torch.tensor([p for row in idx for p in row], dtype=torch.long).pin_memory().to(self.device,
+                                                                                             non_blocking=True)
+        rows = table[ix.view(-1)].view(-1, 2, H).sum(1)
+        embeds = rows[:B * P].view(B, P, H)
+        trail = rows[B * P:].view(B, T, H)
+        mask = torch.tensor([[0] * (P - len(s)) + [1] * len(s) for s in seqs], dtype=torch.long).pin_memory().to(
+            self.device, non_blocking=True)
+        pad_e = table[pad].view(1, 1, H)
         return embeds, mask, trail, pad_e
 
     # -------------------------------------------------------------------------------- generate
@@ -460,17 +519,21 @@ class TTSModel:
                     side = None
                 # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
                 codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
-                c0 = codes[:, :, 0].cpu()
-                for b in range(B):
-                    if end[b] is None:
-                        hit = (c0[b, scanned:] == eos).nonzero()
-                        if hit.numel():
-                            end[b] = scanned + int(hit[0])
-                    if final and end[b] is None:
-                        end[b] = frames
-                    if end[b] is not None and cap[b] is None:
-                        cap[b] = up * (pre_nz[b] + int((c0[b, :end[b]] != 0).sum()))
-                scanned = frames
+                # the EOS scan reads cb0 on the host (a sync on the frame just launched); columns [0, frames] hold
+                # tokens sampled at n_generated <= frames, and EOS is suppressed below MIN_NEW_TOKENS, so the first
+                # chunk skips the scan and its codec feed is queued right behind the frame
+                if final or frames + 1 > MIN_NEW_TOKENS:
+                    c0 = codes[:, :, 0].cpu()
+                    for b in range(B):
+                        if end[b] is None:
+                            hit = (c0[b, scanned:] == eos).nonzero()
+                            if hit.numel():
+                                end[b] = scanned + int(hit[0])
+                        if final and end[b] is None:
+                            end[b] = frames
+                        if end[b] is not None and cap[b] is None:
+                            cap[b] = up * (pre_nz[b] + int((c0[b, :end[b]] != 0).sum()))
+                    scanned = frames
                 # decode positions (prefix + generated) available for every row; the sequence length once all ended
                 t_end = max(R[b] + end[b] for b in range(B)) if all(x is not None for x in end) else None
                 avail = t_end if t_end is not None else min(R[b] + frames for b in range(B) if end[b] is None)

@@ -131,6 +131,8 @@ PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
 PF = _hip.env_int("QT_PF", 1) != 0  # parsed as the library parses it (C atoi)
 # static prefill buffers (+ captured graphs) kept per session: the most recently used prompt lengths, LRU-evicted
 PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
+# the generation config's min_new_tokens (M:2044-2066): EOS is suppressed while a row has generated fewer tokens
+MIN_NEW_TOKENS = 2
 
 
 def _lru_get(d: OrderedDict, key):
@@ -359,6 +361,16 @@ class TalkerEngine:
         ids = _to_dev_i32(ids, self.dev)
         n = ids.numel()
         thd = self.text_emb.shape[1]
+        if n > 16 and self.text_emb.dtype == torch.bfloat16 and self.fc1.dtype == torch.bfloat16:
+            # a batch's prompt text (~1.7k ids at B = 8 x 200 tokens): gather the rows, then the bf16-A prefill GEMMs
+            # (the gathered-A path is the generic gemm_wt: 240 us for fc1 at B = 8); fc1's output is stored in bf16,
+            # the value fc2's MFMA reads either way
+            a16 = self.text_emb.index_select(0, ids)  # bf16 rows, as stored
+            h16 = torch.empty(n, self.fc1.N, dtype=torch.bfloat16, device=self.dev)
+            K.gemm(a16, self.fc1, h16, n, thd, self.fc1.N, act=_hip.ACT_SILU)
+            out = torch.empty(n, self.fc2.N, dtype=torch.float32, device=self.dev)
+            K.gemm(h16, self.fc2, out, n, self.fc1.N, self.fc2.N)
+            return out
         h = torch.empty(n, self.fc1.N, dtype=torch.float32, device=self.dev)
         K.gemm(self.text_emb, self.fc1, h, n, thd, self.fc1.N, a_dtype=self.text_emb.dtype, a_index=ids,
                act=_hip.ACT_SILU)
@@ -432,7 +444,7 @@ class TalkerEngine:
         b1 = s.B if b1 is None else b1
         Hc = self.cp.H
         K.sample(logits[b0:b1], b1 - b0, self.V, self.V, s.tok0[b0:b1], seen=s.seen[b0:b1],
-                 rep_penalty=gp.repetition_penalty, n_generated=s.n_gen[b0:b1], min_new_tokens=2, eos_id=eos,
+                 rep_penalty=gp.repetition_penalty, n_generated=s.n_gen[b0:b1], min_new_tokens=MIN_NEW_TOKENS, eos_id=eos,
                  suppress=(self.V - 1024, self.V, self.tc["codec_eos_token_id"]), ignore_eos=gp.ignore_eos,
                  finished=s.finished[b0:b1], do_sample=gp.do_sample, top_k=gp.top_k, top_p=gp.top_p,
                  temperature=gp.temperature, seed_ptr=s.seed, step=s.step[b0:b1], substep=substep,

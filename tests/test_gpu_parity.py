@@ -181,6 +181,34 @@ def test_igemm_conv_bf16(cin, cout, k, dil, T, snake):
     torch.testing.assert_close(got, ref + res, atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("cin,cout,k,dil,T,B,elu", [(1024, 1536, 7, 1, 6, 8, False), (192, 96, 7, 9, 30, 2, False),
+                                                   (64, 40, 3, 3, 17, 3, True), (96, 64, 1, 1, 40, 4, False)])
+@pytest.mark.parametrize("snake", [False, True])
+def test_short_window_conv_im2col(cin, cout, k, dil, T, B, elu, snake):
+    """Short conv windows (<= 256 rows: a streamed codec window's early stages) go through im2col + the linear GEMMs:
+    same result as the implicit-GEMM path (splitk=1 keeps igemm_k) and as torch conv1d on the same bf16 operands."""
+    from qwen_tts import kernels as Kn, _hip
+    dev = _dev()
+    Kn.gemm_workspace(dev)
+    g = torch.Generator().manual_seed(cin + cout + k + T)
+    w, b = torch.randn(cout, cin, k, generator=g) * 0.03, torch.randn(cout, generator=g) * 0.1
+    x = _bf(torch.randn(B, cin, T, generator=g))
+    al, ib = torch.exp(0.3 * torch.randn(cin, generator=g)), torch.exp(-0.3 * torch.randn(cin, generator=g))
+    xin = torch.nn.functional.elu(x) if elu else x
+    xin = _bf(_snake_ref(xin, al, ib)) if snake else _bf(xin)
+    ref = torch.nn.functional.conv1d(torch.nn.functional.pad(xin, ((k - 1) * dil, 0)), _bf(w), b, dilation=dil)
+    t = Kn.tile_conv(w.to(dev), b.to(dev), torch.bfloat16, dil)
+    xl = x.permute(0, 2, 1).contiguous().to(dev, torch.bfloat16)
+    outs = []
+    for sk in (0, 1):
+        out = torch.zeros(B * T, cout, device=dev)
+        Kn.gemm(xl, t, out, B * T, cin, cout, conv=(T, T, -(k - 1) * dil, dil), splitk=sk,
+                snake=(al.to(dev), ib.to(dev)) if snake else None, a_act=_hip.AACT_ELU if elu else _hip.AACT_NONE)
+        outs.append(out.view(B, T, cout).permute(0, 2, 1).cpu())
+    torch.testing.assert_close(outs[0], ref, atol=3e-3, rtol=3e-3)
+    torch.testing.assert_close(outs[0], outs[1], atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("s", [2, 5, 8])
 def test_igemm_transposed_conv_bf16(s):
     from qwen_tts import kernels as Kn
