@@ -946,7 +946,8 @@ inline int sk_max_m() {
 
 // largest row count of a conv routed to im2col + the linear GEMMs (QT_IM2COL_MAX_M, measurement)
 inline int im2col_max_m() {
-  static const int v = [] { const char* e = getenv("QT_IM2COL_MAX_M"); return e ? atoi(e) : 256; }();
+  // (first streamed window at B = 8: 256 rows 1.70 ms, 512 1.39, 1024 1.39, 2048 1.40; profiles/r03_codec_first_window_im2col.txt)
+  static const int v = [] { const char* e = getenv("QT_IM2COL_MAX_M"); return e ? atoi(e) : 1024; }();
   return v;
 }
 
@@ -1117,7 +1118,7 @@ __global__ __launch_bounds__(256) void im2col_k(GemmP p, bf16_t* __restrict__ ou
       u32x4_t{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
 }
 
-// short conv windows (a streamed codec window's early stages: tens of rows, K = taps x cin_pad up to ~7k): igemm_k's
+// short conv windows (<= 1024 rows: a streamed codec window's stages; tens of rows, K = taps x cin_pad up to ~7k): igemm_k's
 // 128-row tiles leave a few dozen blocks each walking hundreds of k chunks (~110-130 us per conv at B = 8 x 1 frame);
 // as im2col + the linear routes (decode GEMV / skinny GEMMs / split-K prefill GEMM) the weights stream over the chip.
 // The im2col image lives in the upper half of the caller's workspace.  QT_IM2COL=0 disables (measurement).

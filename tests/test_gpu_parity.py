@@ -174,11 +174,13 @@ def test_igemm_conv_bf16(cin, cout, k, dil, T, snake):
     res = torch.randn(B, cout, T, generator=g)
     t = Kn.tile_conv(w.to(dev), b.to(dev), torch.bfloat16, dil)
     xl = x.permute(0, 2, 1).contiguous().to(dev, torch.bfloat16)
-    out = res.permute(0, 2, 1).contiguous().reshape(B * T, cout).to(dev)
-    Kn.gemm(xl, t, out, B * T, cin, cout, conv=(T, T, -(k - 1) * dil, dil), epi=_hip.EPI_ADD,
-            snake=(al.to(dev), ib.to(dev)) if snake else None)
-    got = out.view(B, T, cout).permute(0, 2, 1).cpu()
-    torch.testing.assert_close(got, ref + res, atol=2e-3, rtol=2e-3)
+    Kn.gemm_workspace(dev)
+    for sk in (1, 0):  # splitk=1: the implicit GEMM; 0: windows of <= 1024 rows as im2col + the linear GEMMs
+        out = res.permute(0, 2, 1).contiguous().reshape(B * T, cout).to(dev)
+        Kn.gemm(xl, t, out, B * T, cin, cout, conv=(T, T, -(k - 1) * dil, dil), epi=_hip.EPI_ADD,
+                snake=(al.to(dev), ib.to(dev)) if snake else None, splitk=sk)
+        got = out.view(B, T, cout).permute(0, 2, 1).cpu()
+        torch.testing.assert_close(got, ref + res, atol=2e-3, rtol=2e-3)
 
 
 @pytest.mark.parametrize("cin,cout,k,dil,T,B,elu", [(1024, 1536, 7, 1, 6, 8, False), (192, 96, 7, 9, 30, 2, False),
