@@ -119,6 +119,12 @@ class _Stack:
 # code-predictor decode steps: qt_decode_attn_oproj (attention fused into o_proj + residual); QT_ATTN_OPROJ=0 keeps
 # the two-launch path (decode attention, then the o_proj GEMV) for A/B measurement
 ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
+# ... for lanes of at most this many rows: every block of the fused kernel re-reads its o_proj weight slice per row
+# (R x 4 MiB through L2 per launch), so at 64 rows it took 50.5 us per launch (bench --workload vd64 profile).
+# vd64 audio-s/s with 16 / 32 / 64 refilled rows: fused 238 / 285 / 328, two launches 254 / 337 / 452
+# (profiles/r03_attn_oproj_rows_ab.txt); at 8 rows the fused launch wins (round 2: 155.9 -> 164.0).  QT_ATTN_OPROJ_MAX
+# overrides (A/B)
+ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -183,7 +189,7 @@ class CPLane:
         self.x = s.cp_x[2 * b0:2 * b1]
         self.x16 = None if s.cp_x16 is None else s.cp_x16[2 * b0:2 * b1]
         self.kv = ([k[b0:b1] for k in s.cp_kv[0]], [v[b0:b1] for v in s.cp_kv[1]])
-        self.sc = _scratch(2 * nb, c, dev, attn_oproj=True)
+        self.sc = _scratch(2 * nb, c, dev, attn_oproj=nb <= ATTN_OPROJ_MAX)
         self.ws = ws
         self.logits = torch.zeros(nb, eng.Vc, dtype=torch.float32, device=dev)
         self.tok = s.cp_tok[b0:b1]
