@@ -940,7 +940,12 @@ inline int gemv_mr() {
 
 // largest row count served by the skinny GEMM gemm_sk_k (QT_SK=0 disables it: measurement)
 inline int sk_max_m() {
-  static const int v = [] { const char* e = getenv("QT_SK"); return (e && atoi(e) == 0) ? 0 : 64; }();
+  static const int v = [] {
+    const char* e = getenv("QT_SK");
+    if (e && atoi(e) == 0) return 0;
+    const char* m = getenv("QT_SK_MAX_M");  // (measurement)
+    return m ? std::min(atoi(m), 64) : 48;  // (48 vs 64: bench --workload vd64 451 vs 442 audio-s/s)
+  }();
   return v;
 }
 
@@ -1245,7 +1250,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   bool skinny_gemv = false;
   if (skinny) {
     if (a->N >= 4096) {
-      if (a->M <= 48 && (long long)a->N * a->K <= (8ll << 20) && sk_max_m() >= a->M) p.sk = 1;
+      if (a->M <= sk_max_m() && (long long)a->N * a->K <= (8ll << 20)) p.sk = 1;
       else p.pf_small = 1;
     } else if ((long long)a->M * a->N * a->K <= (400ll << 20)) {
       skinny_gemv = true;
