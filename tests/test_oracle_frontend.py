@@ -3,8 +3,9 @@
 Golden vectors: tests/golden/frontend_{tiny,full}.npz, written by tests/golden/make_golden.py (--only frontend),
 which runs the reference `Qwen3TTSTokenizerV2Model.encode` (transformers MimiModel inside) and
 `mel_spectrogram` + `Qwen3TTSSpeakerEncoder` via `extract_speaker_embedding` on seeded synthetic weights.
-The slaney mel filterbank (librosa, absent offline) is the oracle's restatement on both sides: the filterbank
-itself is parity-unpinned; STFT, mel product, log and the whole ECAPA network are pinned.  CPU only.
+The slaney mel filterbank (librosa, absent offline) is the oracle's restatement on both sides of those fixtures; the
+filterbank itself is pinned separately against the two librosa.filters.mel outputs the reference ships as data
+(tests/golden/librosa_mel_filters.npz, tests/golden/copy_librosa_mel.py).  CPU only.
 """
 import json
 import os
@@ -41,6 +42,17 @@ def test_slaney_filterbank_properties():
     assert (np.diff(peaks) >= 0).all()  # band centres increase
     nz = [np.nonzero(r)[0] for r in w]
     assert all(len(z) and z[-1] - z[0] + 1 == len(z) for z in nz)  # one contiguous triangle per band
+
+
+@pytest.mark.parametrize("n_mels", [80, 128])
+def test_slaney_filterbank_matches_librosa_output(n_mels):
+    """Oracle and product filterbanks == librosa.filters.mel(sr=16000, n_fft=400, n_mels) as the reference stores it
+    (qwen_tts/core/tokenizer_25hz/vq/assets/mel_filters.npz; generating call at whisper_encoder.py:47-53): bit-exact
+    float32."""
+    from qwen_tts.speaker import mel_filterbank
+    ref = np.load(os.path.join(GOLD, "librosa_mel_filters.npz"))[f"mel_{n_mels}"]
+    np.testing.assert_array_equal(slaney_mel_filterbank(16000, 400, n_mels), ref)
+    np.testing.assert_array_equal(mel_filterbank(16000, 400, n_mels, 0.0, 8000.0), ref)
 
 
 @pytest.mark.parametrize("preset,kind,fname", CASES)
