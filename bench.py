@@ -294,8 +294,6 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=24)
     ap.add_argument("--roofline", type=int, default=1)
-    ap.add_argument("--row-groups", type=int, default=1,
-                    help="decode the per-GPU batch as this many concurrent row groups (streams)")
     ap.add_argument("--workload", default="cv8", choices=["cv8", "vd64"],
                     help="cv8: configs[2] (default, weak scaling: 8 x 200-token CustomVoice utterances per GPU); vd64: "
                          "configs[3] (strong scaling: 64 mixed-length VoiceDesign requests LPT-sharded over the ranks)")
@@ -328,7 +326,6 @@ def main():
                                         weights=W, codec_weights=CW)
     del W, CW
     torch.cuda.empty_cache()
-    tts.model.engine.row_groups = a.row_groups
     B = a.batch
     ids = [synth_ids(a.prompt_tokens, rank * 1000 + i) for i in range(B)]
     spk = (["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"] * 8)[:B]

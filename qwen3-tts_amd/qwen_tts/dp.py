@@ -29,7 +29,8 @@ def broadcast_weights(W: Dict[str, torch.Tensor], src: int = 0, group=None, buck
     """In-place broadcast of a state dict (same names / shapes / dtypes on every rank), coalesced: tensors of one
     dtype are packed in name order into flat buckets of <= bucket_bytes and each bucket is one collective (a few
     calls of ~1 GiB instead of one per tensor: xGMI ring broadcasts are bandwidth-bound per link, so large messages
-    run at link speed while hundreds of small ones pay the per-call latency).  Returns the number of collectives."""
+    run at link speed while hundreds of small ones pay the per-call latency).  src is a GLOBAL rank (as
+    torch.distributed.broadcast takes it), also when `group` is a subgroup.  Returns the number of collectives."""
     calls = 0
     by_dtype: Dict[torch.dtype, List[str]] = {}
     for k in sorted(W):
@@ -46,7 +47,7 @@ def broadcast_weights(W: Dict[str, torch.Tensor], src: int = 0, group=None, buck
             flat = torch.cat([W[k].reshape(-1) for k in part]) if len(part) > 1 else W[part[0]].reshape(-1).clone()
             dist.broadcast(flat, src, group=group)
             calls += 1
-            if dist.get_rank(group) != src:
+            if dist.get_rank() != src:  # global ranks on both sides (a subgroup's local numbering may differ)
                 off = 0
                 for k in part:
                     n = W[k].numel()
@@ -58,10 +59,11 @@ def broadcast_weights(W: Dict[str, torch.Tensor], src: int = 0, group=None, buck
 
 
 def gather_results(local: list, indices: List[int], total: int, dst: int = 0, group=None):
-    """Host-side gather of per-rank results back into global order on `dst` (None elsewhere)."""
+    """Host-side gather of per-rank results back into global order on `dst`, a GLOBAL rank as
+    torch.distributed.gather_object takes it (None elsewhere)."""
     world = dist.get_world_size(group)
     payload = list(zip(indices, local))
-    objs = [None] * world if dist.get_rank(group) == dst else None
+    objs = [None] * world if dist.get_rank() == dst else None
     dist.gather_object(payload, objs, dst=dst, group=group)
     if objs is None:
         return None
@@ -106,7 +108,7 @@ def dp_generate(model, input_ids, languages, speakers=None, instruct_ids=None, f
     model: a qwen_tts.model.TTSModel on this rank's GPU.  frames: optional per-request frame caps (known lengths /
     estimates); request i then stops after min(frames[i], max_new_tokens - 1) frames or at its EOS.  Each request
     draws Philox stream i (its global index), so sampled results do not depend on the rank count.
-    Returns (codes list [F_i, 16], wavs list or None) on rank 0 (every rank when gather=False returns its own
+    Returns (codes list [F_i, 16], wavs list or None) on the group's rank 0 (every rank when gather=False returns its own
     share as {index: (codes, wav)}), None on other ranks."""
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
@@ -132,7 +134,9 @@ def dp_generate(model, input_ids, languages, speakers=None, instruct_ids=None, f
     if world == 1:
         res = [local[i] for i in range(n)]
     else:
-        res = gather_results([local[i] for i in mine], mine, n, group=group)
+        # rank 0 of `group`, as a global rank (the collective's dst); the shards above are by group rank
+        dst = dist.get_global_rank(group, 0) if group is not None else 0
+        res = gather_results([local[i] for i in mine], mine, n, dst=dst, group=group)
         if res is None:
             return None
     return [c for c, _ in res], ([w for _, w in res] if decode else None)

@@ -6,6 +6,7 @@ the current stream, so the calls are capturable into HIP graphs.
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -108,7 +109,16 @@ def tile_transconv(w, b, dtype, stride):
 
 
 _WS = {}
-_ACTIVE_WS = []
+# workspaces selected by `use_workspace`, a stack per host thread: two threads issuing on different streams each
+# route their GEMMs through their own workspace (a module-global stack would hand one thread's ws to the other)
+_TLS = threading.local()
+
+
+def _active_stack():
+    st = getattr(_TLS, "ws", None)
+    if st is None:
+        st = _TLS.ws = []
+    return st
 
 
 WS_BYTES = 16 << 20  # >= GEMM_WS_MIN: room for gemm_pf2_k's split-K records of the 17+-row linears
@@ -142,16 +152,23 @@ def side_stream(device):
 
 
 class use_workspace:
-    """`with use_workspace(ws):` routes decode-GEMV split-K through `ws` (e.g. one per row-group stream)."""
+    """`with use_workspace(ws):` routes this host thread's qt_gemm calls (split-K records, im2col images) through
+    `ws` -- one workspace per stream that can run concurrently (a session's, a codec stream slot's).  The selection
+    is per host thread; without one the device's default workspace (single-stream callers) is used."""
 
     def __init__(self, ws):
         self.ws = ws
 
     def __enter__(self):
-        _ACTIVE_WS.append(self.ws)
+        _active_stack().append(self.ws)
 
     def __exit__(self, *exc):
-        _ACTIVE_WS.pop()
+        _active_stack().pop()
+
+
+def active_workspace(device):
+    st = _active_stack()
+    return st[-1] if st else _WS.get(torch.device(device).index or 0)
 
 
 def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=None, eps=0.0, rms=False, colscale=None,
@@ -176,7 +193,7 @@ def gemm(A, W: Tiled, out, M, lda, ldo, *, a_dtype=None, o_dtype=None, gamma=Non
     a.a_act = a_act
     if out2 is not None:
         a.out2, a.ldo2 = ptr(out2), ldo if ldo2 is None else ldo2
-    ws = _ACTIVE_WS[-1] if _ACTIVE_WS else _WS.get(out.device.index or 0)
+    ws = active_workspace(out.device)
     if ws is not None:  # (convs: the short-window im2col route keeps its image in the workspace's upper half)
         a.ws, a.ws_bytes, a.splitk = ptr(ws), ws.numel(), splitk
     if W.taps:

@@ -360,10 +360,17 @@ class TTSModel:
         # a side stream before the (host-bound) prompt assembly, so it runs beside it instead of beside the prefill
         started = self._start_ref_decode(dec, prefix, len(prefix)) if prefix is not None and left_context is None \
             else None
-        emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids, non_streaming_mode,
-                                                   voice_clone_prompt, ref_ids)
-        gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
-                       subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
+        try:
+            emb, mask, trail, pad = self.build_prompts(input_ids, languages, speakers, instruct_ids,
+                                                       non_streaming_mode, voice_clone_prompt, ref_ids)
+            gp = GenParams(max_new_tokens, do_sample, top_k, top_p, temperature, subtalker_dosample, subtalker_top_k,
+                           subtalker_top_p, subtalker_temperature, eos_token_id, repetition_penalty, ignore_eos, seed)
+        except BaseException:
+            # the side-stream reference decode holds a pooled codec slot: hand it back before the error propagates
+            if started is not None:
+                torch.cuda.current_stream(self.device).wait_stream(started[1])
+                started[2].close()
+            raise
         eos = self.engine.tc["codec_eos_token_id"]
         B = emb.shape[0]
         emitted = 0                       # windows [0, emitted) decoded for every row

@@ -175,10 +175,9 @@ def _attn_oproj_ok(st: _Stack) -> bool:
 
 
 class CPLane:
-    """Rows [b0, b1) of a session's code predictor: one independent chain of the 15 sequential CP steps.  A
-    session's lanes run on concurrent streams inside the captured frame graph (fork after the talker's token choice,
-    join before the next talker step): the CP is latency-bound, so two half-batch chains overlap their kernel
-    latencies, and each kernel sees M = B / lanes rows (the decode GEMV folds its activation fetch accordingly)."""
+    """Buffers of a session's code predictor (rows [b0, b1) = the whole batch): the chain of the 15 sequential CP
+    steps of one frame.  (Round 2 also ran half-batch lanes on forked streams inside the frame graph; graph branches
+    do not overlap on this stack and the split measured slower -- 156.5 vs 167.0 audio-s/s -- so it was removed.)"""
 
     def __init__(self, s: "Session", eng: "TalkerEngine", b0: int, b1: int, ws):
         c, dev = eng.cp, eng.dev
@@ -285,16 +284,12 @@ class Session:
         self.pad_embed = f32(t.H)
         self.ws = K.new_workspace(dev)  # split-K scratch private to this session's stream
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox key, read by the captured samplers
-        self.row_base = 0
         self.graph = None
         # prompt length P -> static prefill buffers (+ captured graph once P repeats); LRU, PREFILL_CACHE lengths
         self.prefill = OrderedDict()
         self.slot_prefill = OrderedDict()  # P -> static single-request prefill buffers (serve() refills); LRU
         self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
-        nl = max(1, min(eng.cp_lanes, B))
-        cuts = [B * i // nl for i in range(nl + 1)]
-        self.cp_lanes = [CPLane(self, eng, cuts[i], cuts[i + 1], self.ws if i == 0 else K.new_workspace(dev))
-                         for i in range(nl)]
+        self.cp = CPLane(self, eng, 0, B, self.ws)
 
 
 class TalkerEngine:
@@ -343,13 +338,6 @@ class TalkerEngine:
                 K.gemm(t16, L0.qkv, out, tab.shape[0], Hc, c.qkv_w, rms=True, eps=c.eps)
                 self.cp_qkv_tabs.append(out)
         self._sessions: Dict[tuple, List[Session]] = {}
-        self._streams: List[torch.cuda.Stream] = []
-        # decode row groups: the batch is split into this many independent groups, each with its own session,
-        # HIP stream and captured frame graph; their latency-bound frames overlap on the GPU
-        self.row_groups = int(os.environ.get("QT_ROW_GROUPS", "1"))
-        # code-predictor lanes per session (CPLane): concurrent CP chains inside one frame graph
-        self.cp_lanes = int(os.environ.get("QT_CP_LANES", "1"))
-        self._cp_streams: List[torch.cuda.Stream] = []
         torch.cuda.synchronize()
 
     def _proj_table(self, emb, Hc):
@@ -399,12 +387,12 @@ class TalkerEngine:
         return out
 
     # ---------------------------------------------------------------- sessions / graph
-    def session(self, B, P, max_frames, gp: GenParams, row_base: int = 0, teacher: bool = False) -> Session:
+    def session(self, B, P, max_frames, gp: GenParams, teacher: bool = False) -> Session:
         """A free session of this shape, marked busy (release() hands it back).  A session held by a live request
         (e.g. a suspended stream() generator) is never shared: a concurrent request of the same shape gets a
         session of its own (own KV cache, counters and captured graph)."""
         P_cap = max(64, (P + 63) // 64 * 64)
-        key = (B, max_frames, gp.key(), row_base, teacher)
+        key = (B, max_frames, gp.key(), teacher)
         pool = self._sessions.setdefault(key, [])
         for s in pool:
             if not s.busy and s.P_cap >= P:
@@ -421,7 +409,6 @@ class TalkerEngine:
         for k in [k for k, v in self._sessions.items() if not v and k != key]:
             del self._sessions[k]
         s = Session(self, B, P_cap, max_frames, gp, teacher=teacher)
-        s.row_base = row_base
         self.talker.ensure_rope(s.Lmax + 4, self.dev)
         self._sessions.setdefault(key, []).append(s)
         s.busy = True
@@ -434,11 +421,6 @@ class TalkerEngine:
 
     def all_sessions(self) -> List[Session]:
         return [s for ss in self._sessions.values() for s in ss]
-
-    def _stream(self, i):
-        while len(self._streams) <= i:
-            self._streams.append(torch.cuda.Stream(device=self.dev))
-        return self._streams[i]
 
     def _eos(self, gp):
         return gp.eos_token_id if gp.eos_token_id is not None else self.tc["codec_eos_token_id"]
@@ -464,22 +446,7 @@ class TalkerEngine:
         """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
         B, t = s.B, self.talker
         codes_ld = s.codes.shape[1] * self.G
-        lanes = s.cp_lanes
-        if len(lanes) == 1:
-            self._cp_lane(s, lanes[0])
-        else:  # fork: lanes 1.. on their own streams, lane 0 on the frame's stream; join before the talker step
-            main = torch.cuda.current_stream(self.dev)
-            while len(self._cp_streams) < len(lanes) - 1:
-                self._cp_streams.append(torch.cuda.Stream(device=self.dev))
-            for i in range(1, len(lanes)):
-                st = self._cp_streams[i - 1]
-                st.wait_stream(main)
-                with torch.cuda.stream(st), K.use_workspace(lanes[i].ws):
-                    self._cp_lane(s, lanes[i])
-            with K.use_workspace(lanes[0].ws):
-                self._cp_lane(s, lanes[0])
-            for i in range(1, len(lanes)):
-                main.wait_stream(self._cp_streams[i - 1])
+        self._cp_lane(s, s.cp)
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
@@ -530,16 +497,13 @@ class TalkerEngine:
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,
                              tts_pad: torch.Tensor, gp: GenParams, use_graph: bool = True, on_frames=None,
-                             groups: Optional[int] = None, philox_ids=None):
+                             philox_ids=None):
         """embeds fp32 [B,P,H] left-padded, mask [B,P] -> (codes list [F_i,16] int64 cpu, hidden list).
 
-        The batch is decoded as `groups` independent row groups (default self.row_groups), each on its own
-        HIP stream with its own session and captured frame graph; per-row arithmetic (and, through row_base,
-        each row's Philox stream) is the same as decoding the batch whole.  philox_ids: optional per-row Philox
-        stream ids (default the row index) -- a data-parallel shard passes its requests' global indices, so every
-        request draws the same stream whichever rank and row decode it."""
+        philox_ids: optional per-row Philox stream ids (default the row index) -- a data-parallel shard passes its
+        requests' global indices, so every request draws the same stream whichever rank and row decode it."""
         it = self.decode_iter(embeds, mask, trailing, tts_pad, gp, use_graph=use_graph, on_frames=on_frames,
-                              groups=groups, philox_ids=philox_ids)
+                              philox_ids=philox_ids)
         out = None
         for sessions, frames, final in it:
             if final:  # collected while the sessions are still held by this request
@@ -577,34 +541,25 @@ class TalkerEngine:
             self.release([s])
 
     def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
-                    groups: Optional[int] = None, every: int = 0, first: int = 0, grow: bool = False,
-                    philox_ids=None):
+                    every: int = 0, first: int = 0, grow: bool = False, philox_ids=None):
         """Prefill + frame loop as a generator: yields (sessions, frames_done, final) after `first` frames, then
         every `every` frames (0: only at the end; grow=True: intervals double from first - 1 up to `every`), and once
-        at the end with final=True.  codes[:, :frames_done]
-        of every session are final when yielded (device; the yield synchronises the row-group streams), and
-        codes[:, frames_done, 0] already holds the next frame's cb0 (EOS of rows that just finished)."""
+        at the end with final=True.  `sessions` is a one-element list (the batch's session); codes[:, :frames_done]
+        are final when yielded (device), and codes[:, frames_done, 0] already holds the next frame's cb0 (EOS of rows
+        that just finished)."""
         B, P, H = embeds.shape
-        G = max(1, min(groups or self.row_groups, B))
         max_frames = max(gp.max_new_tokens - 1, 0)
         seed = gp.resolve_seed()
-        cuts = [B * i // G for i in range(G + 1)]
         main = torch.cuda.current_stream(self.dev)
-        sessions, streams = [], []
+        sessions = []
         try:
-            for gi in range(G):
-                b0, b1 = cuts[gi], cuts[gi + 1]
-                st = self._stream(gi) if G > 1 else main
-                st.wait_stream(main)
-                s = self.session(b1 - b0, P, max(max_frames, 1), gp, row_base=b0)
-                sessions.append(s)
-                with torch.cuda.stream(st), K.use_workspace(s.ws):
-                    self._prefill(s, embeds[b0:b1], mask[b0:b1], trailing[b0:b1], tts_pad, seed,
-                                  None if philox_ids is None else philox_ids[b0:b1])
-                    if max_frames > 0 and use_graph and s.graph is None:
-                        s.graph = self._capture(s)
-                streams.append(st)
-            yield from self._frames(sessions, streams, max_frames, use_graph, on_frames, every, first, grow)
+            s = self.session(B, P, max(max_frames, 1), gp)
+            sessions.append(s)
+            with K.use_workspace(s.ws):
+                self._prefill(s, embeds, mask, trailing, tts_pad, seed, philox_ids)
+                if max_frames > 0 and use_graph and s.graph is None:
+                    s.graph = self._capture(s)
+            yield from self._frames(sessions, [main], max_frames, use_graph, on_frames, every, first, grow)
         finally:
             self.release(sessions)
 
@@ -828,7 +783,7 @@ class TalkerEngine:
 
     def _prefill(self, s: Session, embeds, mask, trailing, tts_pad, seed: int, philox_ids=None):
         """Talker prefill of one row group (M:1746-1800 positions, M:2044 first token) into session s.
-        philox_ids: per-row Philox stream ids (default row_base + row)."""
+        philox_ids: per-row Philox stream ids (default the row index)."""
         B, P, H = embeds.shape
         t = self.talker
         dev = self.dev
@@ -837,7 +792,7 @@ class TalkerEngine:
             z.zero_()
         s.seed.fill_(seed)
         if philox_ids is None:
-            torch.arange(s.row_base, s.row_base + B, dtype=torch.int32, device=dev, out=s.prow)
+            torch.arange(B, dtype=torch.int32, device=dev, out=s.prow)
         else:
             s.prow.copy_(_to_dev_i32(list(philox_ids), dev))
         # stale K/V beyond each row's valid range is never read (row_start/row_len bound every read)

@@ -115,3 +115,41 @@ def test_world2_dp_generate_shards_and_gathers():
     loads = [sum(100 * frames[i] for i in c[0]["philox_ids"]) for c in (calls0, got[1][1])]
     assert abs(loads[0] - loads[1]) <= 100 * max(frames)
     assert ncalls == 4  # fp32 a+b (<= 500 B), fp32 c, int64 d, bf16 e
+
+
+def _subgroup_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qwen_tts.dp import dp_generate
+    grp = dist.new_group([1, 2])  # collective on every rank; group-local ranks 0, 1 = global ranks 1, 2
+    res = None
+    if rank in (1, 2):
+        ref = {"w": torch.arange(6, dtype=torch.float32) + 10.0}
+        # global src 1 is group-local rank 0: rank 2 (local 1) must receive, rank 1 keeps its copy
+        W = {"w": ref["w"].clone() if rank == 1 else torch.zeros(6)}
+        broadcast_weights(W, src=1, group=grp)
+        ids = [torch.zeros(1, n) for n in (5, 9, 3, 7)]
+        out = dp_generate(_StubModel(), ids, ["english"] * 4, None, None, frames=[4, 9, 2, 6], slots=2,
+                          max_new_tokens=64, group=grp)
+        res = (torch.equal(W["w"], ref["w"]), None if out is None else [int(c[0, 0]) for c in out[0]])
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_world3_subgroup_uses_global_ranks():
+    """A subgroup whose local numbering differs from the global one ([1, 2]): the weight broadcast from global rank 1
+    reaches global rank 2, and dp_generate gathers to the group's first rank (global 1) in request order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(3))
+    for p in ps:
+        p.join(timeout=60)
+    assert got[0] is None
+    assert got[1] == (True, [0, 1, 2, 3])
+    assert got[2] == (True, None)

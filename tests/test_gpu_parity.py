@@ -926,53 +926,6 @@ def test_talker_eos_ragged_bit_exact(tiny_models):
         np.testing.assert_array_equal(c.numpy(), z[f"eos_b2/codes{j}"])
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_row_groups_identical_to_whole_batch(tiny_models, dtype):
-    """Decoding the batch as 2 or 3 concurrent row groups (own stream / session / graph each) reproduces the
-    whole-batch codes exactly, sampling included (Philox stream id = row_base + row)."""
-    from cases import talker_cases
-    from qwen_tts.model import TTSModel
-    cfg, W, _ = tiny_models["tiny-customvoice"]
-    model = TTSModel(cfg, W, dtype=dtype)
-    case = dict(talker_cases()["cv_b3_auto_nospk"], do_sample=True, subtalker_dosample=True, seed=5)
-    ref = None
-    for groups in (1, 2, 3):
-        model.engine.row_groups = groups
-        codes, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg)
-        if ref is None:
-            ref = codes
-            continue
-        assert len(codes) == len(ref)
-        for a, b in zip(codes, ref):
-            np.testing.assert_array_equal(a.numpy(), b.numpy())
-
-
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_cp_lanes_identical_to_one_chain(tiny_models, dtype):
-    """The code predictor as 2 or 3 concurrent lanes (CPLane: forked streams inside the frame graph, graph and
-    eager) reproduces the single-chain codes exactly, sampling included."""
-    from cases import talker_cases
-    from qwen_tts.model import TTSModel
-    cfg, W, _ = tiny_models["tiny-customvoice"]
-    model = TTSModel(cfg, W, dtype=dtype)
-    case = dict(talker_cases()["cv_b3_auto_nospk"], do_sample=True, subtalker_dosample=True, seed=7)
-    ref = None
-    try:
-        for lanes, use_graph in ((1, True), (2, True), (3, True), (2, False)):
-            model.engine.cp_lanes = lanes
-            model.engine._sessions.clear()
-            codes, _ = _run_case(model, "cv_b3_auto_nospk", case, 2, cfg, use_graph=use_graph)
-            if ref is None:
-                ref = codes
-                continue
-            assert len(codes) == len(ref)
-            for a, b in zip(codes, ref):
-                np.testing.assert_array_equal(a.numpy(), b.numpy())
-    finally:
-        model.engine.cp_lanes = 1
-        model.engine._sessions.clear()
-
-
 @pytest.mark.parametrize("ctx,eos,frames", [(None, False, 30), (None, True, 24), (None, False, 331), (1000, False, 30),
                                             (1000, True, 24), (2, True, 24), (1000, False, 331)])
 def test_stream_matches_one_shot(tiny_models, ctx, eos, frames):
@@ -1375,6 +1328,37 @@ def test_stream_voice_clone_matches_wrapper(tiny_models, frames, both):
         got = np.concatenate(chunks[b])
         assert got.shape == want.shape, (b, got.shape, want.shape)
         np.testing.assert_allclose(got, want, atol=2e-4, rtol=0)
+
+
+def test_stream_voice_clone_bad_request_releases_codec_slot(tiny_models):
+    """stream() starts the reference-frame codec decode (a pooled CodecStream slot) before the prompt assembly; a
+    request the assembly rejects (unknown language -> NotImplementedError, as the reference) must hand the slot back,
+    so repeated bad requests do not grow the pool."""
+    from cases import gen_kwargs, make_inputs, talker_cases
+    from oracle import codec_param_specs, load_preset, synth_state_dict
+    from qwen_tts import Qwen3TTSTokenizer
+    _dev()
+    cfg, W, model = tiny_models["tiny-customvoice"]
+    _, ccfg = load_preset("tiny-customvoice")
+    CW = {k: torch.from_numpy(v) for k, v in synth_state_dict(codec_param_specs(ccfg)).items()}
+    tok = Qwen3TTSTokenizer.from_pretrained("synthetic:tiny-customvoice/speech_tokenizer", dtype="fp32", weights=CW)
+    model.load_speech_tokenizer(tok)
+    key = "icl_b2"
+    case = dict(talker_cases()[key], max_new_tokens=6)
+    case["icl"] = [(5, 7, True, False), (12, 4, True, False)]
+    ids, ins, vcp, ref_ids = make_inputs(case, list(talker_cases()).index(key), cfg["talker_config"]["hidden_size"])
+    kw = dict(input_ids=ids, instruct_ids=ins, ref_ids=ref_ids, voice_clone_prompt=vcp, speakers=case["speakers"],
+              non_streaming_mode=case["non_streaming_mode"], **gen_kwargs(case))
+    dec = model.speech_tokenizer.model
+    for _ in range(3):
+        with pytest.raises(NotImplementedError):
+            next(iter(model.stream(languages=["klingon"] * len(ids), **kw)))
+    torch.cuda.synchronize()
+    slots = [sl for pool in dec._slots.values() for sl in pool]
+    assert slots and not any(sl.busy for sl in slots)
+    assert len(slots) == 1  # the one slot was reused by every attempt
+    out = list(model.stream(languages=case["languages"], **kw))  # and a good request still streams
+    assert out and out[-1][2]
 
 
 def test_prefill_buffers_lru_bounded(tiny_models):

@@ -24,7 +24,7 @@ def main():
                        seed=1, **gen)
     torch.cuda.synchronize()
     for s in tts.model.engine.all_sessions():
-        for ln in s.cp_lanes:
+        for ln in [s.cp]:
             lg = ln.logits.float().cpu().numpy()[: ln.nb] / 0.9
             for r, row in enumerate(lg):
                 m = row.max()

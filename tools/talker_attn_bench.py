@@ -13,17 +13,18 @@ dev = torch.device("cuda:0")
 
 def main():
     B, hq, hkv, D = 8, 16, 8, 128
-    Lmax = 480
+    Ls = [int(x) for x in os.environ.get("ATTN_L", "138,210,267,340,466").split(",")]
+    Lmax = max(Ls) + 8
     nl = 28  # distinct layer caches: every launch streams its keys from HBM / MALL as in a frame
     kc = [torch.randn(B, hkv, Lmax, D, device=dev).to(torch.bfloat16) for _ in range(nl)]
     vc = [torch.randn(B, hkv, Lmax, D, device=dev).to(torch.bfloat16) for _ in range(nl)]
     qkv = torch.randn(B, (hq + 2 * hkv) * D, device=dev)
     qn = torch.ones(D, device=dev)
-    cos, sin = K.rope_tables(D, 1e6, 4096, dev)
+    cos, sin = K.rope_tables(D, 1e6, Lmax + 8, dev)
     att = torch.zeros(B, hq * D, device=dev, dtype=torch.bfloat16)
     i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
     rb, zero = i32(range(B)), i32([0] * B)
-    for L in [int(x) for x in os.environ.get("ATTN_L", "138,210,267,340,466").split(",")]:
+    for L in Ls:
         pos = i32([L - 1] * B)
         for ns in [int(x) for x in os.environ.get("ATTN_NS", "1,2,4").split(",")]:
             ws = torch.zeros(K.decode_attn_ws_bytes(B, hq, hkv, D, ns), dtype=torch.uint8, device=dev) if ns > 1 else None
