@@ -390,6 +390,12 @@ def process_logits(scores, history, n_generated, eos, suppress, rep_penalty, min
 
 def warp_and_sample(scores, temperature, top_k, top_p, gen: torch.Generator):
     """Temperature -> TopK -> TopP warpers, softmax, multinomial (transformers 4.57 sample path)."""
+    return torch.multinomial(warp_probs(scores, temperature, top_k, top_p), 1, generator=gen).squeeze(1)
+
+
+def warp_probs(scores, temperature, top_k, top_p):
+    """The distribution warp_and_sample draws from: TemperatureLogitsWarper -> TopKLogitsWarper -> TopPLogitsWarper ->
+    softmax (transformers 4.57 `_sample` with do_sample=True)."""
     if temperature is not None and temperature != 1.0:
         scores = scores / temperature
     if top_k is not None and top_k != 0:
@@ -402,8 +408,7 @@ def warp_and_sample(scores, temperature, top_k, top_p, gen: torch.Generator):
         rm = cp <= (1 - top_p)
         rm[..., -1:] = 0
         scores = scores.masked_fill(rm.scatter(1, si, rm), -math.inf)
-    probs = torch.softmax(scores, -1)
-    return torch.multinomial(probs, 1, generator=gen).squeeze(1)
+    return torch.softmax(scores, -1)
 
 
 @dataclass

@@ -287,6 +287,83 @@ def make_full(only=None):
         np.savez_compressed(os.path.join(HERE, f"full_{key}.npz"), **out)
 
 
+class _TeacherForcer:
+    """Teacher forcing inside the reference's own generate() (process-local, this script only): every call of a
+    LogitsProcessorList -- the talker's (vocab V_t) once per frame and the code predictor's (vocab V_c) 15 times per
+    frame, in that order (M:1671-1680, 2272) -- records the argmax of the processed scores, then returns scores that
+    make the greedy argmax pick the fp32 reference's token instead, so every step sees the fp32 reference history.
+    picks[b, f, g] is the reference model's own choice at frame f, codebook g (the codes' layout)."""
+
+    def __init__(self, ref_codes, v_talker, v_cp):
+        self.B, self.F = len(ref_codes), max(int(c.shape[0]) for c in ref_codes)
+        self.ref = np.zeros((self.B, self.F, 16), dtype=np.int64)
+        for b, c in enumerate(ref_codes):
+            self.ref[b, :c.shape[0]] = c
+        self.picks = np.zeros_like(self.ref)
+        self.vt, self.vc = v_talker, v_cp
+        self.t, self.g = 0, 0
+
+    def __call__(self, orig, plist, input_ids, scores, **kw):
+        out = orig(plist, input_ids, scores, **kw)
+        V = out.shape[-1]
+        if V == self.vt:
+            f, col = self.t, 0
+            self.t, self.g = self.t + 1, 0
+        else:
+            assert V == self.vc, V
+            self.g += 1
+            f, col = self.t - 1, self.g
+        pick = out.argmax(-1).cpu().numpy()
+        if f >= self.F:  # past the longest reference row (the generate's trailing step): keep the model's own choice
+            return out
+        self.picks[:, f, col] = pick
+        forced = torch.as_tensor(self.ref[:, f, col], device=out.device)
+        hard = torch.full_like(out, float("-inf"))
+        hard.scatter_(1, forced[:, None], 0.0)
+        return hard
+
+
+def make_full_bf16(only=None):
+    """The reference itself in bf16 (the examples' dtype, examples/test_model_12hz_custom_voice.py:30: parameters cast to
+    bf16 as from_pretrained(dtype=torch.bfloat16) loads them; buffers such as RoPE inv_freq stay fp32), eager CPU, on
+    the full-dim cases cv17_b8_stream and cv06_b1_nonstream: (1) teacher-forced on the fp32 reference codes of
+    full_<key>.npz -- its own greedy pick at every position; (2) free-running greedy codes.  Written to
+    full_<key>_refbf16.npz: the calibration of bf16 agreement (tests/test_gpu_full.py)."""
+    import transformers.generation.logits_process as lp
+    from cases import full_cases
+    for key in ("cv17_b8_stream", "cv06_b1_nonstream"):
+        if only and key != only:
+            continue
+        case = full_cases()[key]
+        t0 = time.time()
+        model, cfg = build_ref_model(case["preset"])
+        for p in model.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        H = cfg["talker_config"]["hidden_size"]
+        z = np.load(os.path.join(HERE, f"full_{key}.npz"))
+        ref = [z[f"codes{j}"] for j in range(int(z["n"]))]
+        tf = _TeacherForcer(ref, cfg["talker_config"]["vocab_size"],
+                            cfg["talker_config"]["code_predictor_config"]["vocab_size"])
+        orig = lp.LogitsProcessorList.__call__
+        lp.LogitsProcessorList.__call__ = lambda self, ids, sc, **kw: tf(orig, self, ids, sc, **kw)
+        try:
+            tcase = dict(case, max_new_tokens=tf.F + 1)
+            run_ref_generate(model, tcase, case["idx"], H)
+        finally:
+            lp.LogitsProcessorList.__call__ = orig
+        agree = np.mean([np.mean(tf.picks[b, :r.shape[0]] == r) for b, r in enumerate(ref)])
+        print(f"  {key}: reference bf16 teacher-forced agreement with its fp32 codes {agree:.4%} "
+              f"({time.time() - t0:.0f}s)")
+        t0 = time.time()
+        codes, _ = run_ref_generate(model, case, case["idx"], H)
+        print(f"  {key}: reference bf16 free-running frames {[c.shape[0] for c in codes]} ({time.time() - t0:.0f}s)")
+        out = {"n": np.array(len(ref)), "picks_tf": tf.picks.astype(np.int32)}
+        for j, c in enumerate(codes):
+            out[f"codes_free{j}"] = c.numpy().astype(np.int32)
+        np.savez_compressed(os.path.join(HERE, f"full_{key}_refbf16.npz"), **out)
+        del model
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true")
@@ -309,8 +386,10 @@ def main():
         # context, and a ragged pair whose long row restarts while the short one is zero padding
         make_codec("1.7b-customvoice", {"t300": [300], "t325": [325], "t700": [700], "ragged_325_40": [325, 40]},
                    "codec_full_chunks.npz", stride=17)
-    if a.full or (a.only or "").startswith("full"):
+    if a.full or ((a.only or "").startswith("full") and not (a.only or "").startswith("full_bf16")):
         make_full(a.only.split(":", 1)[1] if a.only and ":" in a.only else None)
+    if a.full or (a.only or "").startswith("full_bf16"):
+        make_full_bf16(a.only.split(":", 1)[1] if a.only and ":" in a.only else None)
 
 
 if __name__ == "__main__":

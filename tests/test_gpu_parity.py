@@ -742,6 +742,46 @@ def test_sample_fast_topk_distribution(V, k):
     assert bool(((freq - pr).abs() <= 5 * sd + 1e-3).all())
 
 
+@pytest.mark.parametrize("V,k,p,ngen", [(3072, 50, 1.0, 1), (3072, 50, 1.0, 5), (2048, 50, 1.0, 5), (3072, 50, 0.8, 5),
+                                       (2048, 0, 0.9, 5)])
+def test_sample_full_processor_chain_distribution(V, k, p, ngen):
+    """Sampled mode through the whole HF-4.57 chain the bench and the wrapper defaults use (M:2044-2066): repetition
+    penalty 1.05 on the generated history (`seen`), min_new_tokens = 2 (EOS masked while n_generated < 2), the
+    suppress range [V - 1024, V) minus EOS (talker vocab), then temperature 0.9 -> top-k -> top-p -> softmax -> draw.
+    Frequencies of one row repeated R times vs oracle.process_logits -> oracle.warp_probs (5-sigma bound per token);
+    the penalised history sits at the top of the row (it moves the top-k boundary), a suppressed token and EOS carry
+    the largest logits (never drawn / masked below min_new_tokens)."""
+    from qwen_tts import kernels as Kn
+    from oracle.talker import process_logits, warp_probs
+    dev = _dev()
+    R, eos = 16384, V - 1024 + 102
+    g = torch.Generator().manual_seed(V + k + ngen)
+    row = torch.randn(1, V, generator=g) * 1.5
+    top = torch.topk(row, 8, -1).indices[0]
+    hist = torch.cat([top[:5], torch.randint(0, V - 1024, (7,), generator=g)])[None]  # penalised history
+    row[0, V - 1024 + 5] = 9.0   # suppressed: never drawn
+    row[0, eos] = float(row.max()) + 0.5  # EOS: masked while n_generated < min_new_tokens
+    supp = [i for i in range(V - 1024, V) if i != eos] if V == 3072 else []
+    scores = process_logits(row, hist, ngen, eos, supp, 1.05)
+    pr = warp_probs(scores, 0.9, k, p)[0]
+    seen = torch.zeros(R, V, dtype=torch.uint8)
+    seen[:, hist[0]] = 1
+    tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    Kn.sample(row.expand(R, V).contiguous().to(dev), R, V, V, tok, seen=seen.to(dev), rep_penalty=1.05,
+              n_generated=torch.tensor([ngen], dtype=torch.int32, device=dev), min_new_tokens=2, eos_id=eos,
+              suppress=(V - 1024, V, eos) if supp else (0, 0, -1), do_sample=True, top_k=k, top_p=p, temperature=0.9,
+              seed=31 + ngen, step=torch.full((1,), 4, dtype=torch.int32, device=dev), substep=1)
+    t = tok.cpu().long()
+    assert bool((pr[t] > 0).all()), "drew a token outside the processed + warped support"
+    freq = torch.bincount(t, minlength=V).float() / R
+    sd = (pr * (1 - pr) / R).sqrt()
+    assert bool(((freq - pr).abs() <= 5 * sd + 1e-3).all()), float(((freq - pr).abs() - 5 * sd).max())
+    if ngen < 2:
+        assert not bool((t == eos).any())
+    else:
+        assert pr[eos] > 0.01 and abs(freq[eos] - pr[eos]) <= 5 * sd[eos] + 1e-3
+
+
 def test_sample_fast_topk_fallbacks():
     """Shapes the fast path hands back to the block search or must mask: a wave with > 64 tied keys (all scores
     equal: uniform over the whole row, ties kept), and fewer finite scores than k (-inf never drawn)."""
