@@ -53,55 +53,118 @@ def make_weights(preset, dev, world, rank):
     return cfg, W, CW
 
 
-ROOF_KERNEL = "gemv_wt<bf16,bf16,bf16,WPB=4,U=4,rms,fold=2> (talker MLP gate-up decode GEMV, N=12288 K=2048 M=8)"
+def _gemv_entry(name, kernel, n_frame, Ws, M, K, N, a_dtype, o_dtype, dev, rms=False, epi=None, reps=10,
+                extra_bytes=0):
+    """One decode GEMV shape timed live: a HIP graph of one launch per weight in Ws (the model's distinct per-layer
+    weights, as in a frame), replayed `reps` times between HIP events on the capture stream.  Algorithmic bytes per
+    launch = weight tiles + M x K activations + M x N outputs (x2 + the bf16 shadow for a residual add)."""
+    from qwen_tts import _hip, kernels as Kn
+    A = torch.randn(M, K, device=dev).to(a_dtype)
+    out = torch.randn(M, N, device=dev).to(o_dtype)
+    x16 = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if epi == _hip.EPI_ADD else None
+    e = _hip.EPI_STORE if epi is None else epi
+    N_out = N // 2 if e == _hip.EPI_SWIGLU else N
+    if e == _hip.EPI_SWIGLU:
+        out = torch.empty(M, N_out, dtype=o_dtype, device=dev)
+
+    def run():
+        for W in Ws:
+            Kn.gemm(A, W, out, M, K, N_out, rms=rms, eps=1e-6, epi=e, out2=x16)
+    us = _graph_us(run, dev, reps) / len(Ws)
+    w_bytes = Ws[0].w.numel() * Ws[0].w.element_size()
+    o_el = torch.tensor([], dtype=o_dtype).element_size()
+    a_el = torch.tensor([], dtype=a_dtype).element_size()
+    byt = w_bytes + M * K * a_el + M * N_out * o_el * (2 if e == _hip.EPI_ADD else 1) + (M * N_out * 2 if x16 is not None
+                                                                                       else 0) + extra_bytes
+    return dict(name=name, kernel=kernel, bound="hbm", launches_per_frame=n_frame, avg_us=us, bytes=byt)
 
 
-def gateup_bytes(eng, B):
-    """Algorithmic HBM bytes of one talker gate-up launch: bf16 weight tiles + A rows (the bf16 residual shadow in
-    bf16 mode) + bf16 SwiGLU out."""
-    t = eng.talker
-    L = t.layers[0].gu
-    a_bytes = 2 if eng.wdt == torch.bfloat16 else 4
-    return L.w.numel() * L.w.element_size() + B * t.H * a_bytes + B * t.I * L.w.element_size()
+def attn_oproj_entry(tts, B, pos=9, reps=20):
+    """Code-predictor fused attention + o_proj + residual (attn_oproj_k) at cache position `pos` (the mean over the 14
+    decode steps), 5 launches over the 5 layers' distinct o_proj weights per replay.  Algorithmic bytes per launch =
+    o_proj weights + K/V of (pos + 1) keys + the q/k/v rows read + the residual read and written (fp32 + bf16)."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    c, dev = eng.cp, eng.dev
+    kc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    vc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    qkv = torch.randn(B, c.qkv_w, device=dev)
+    x = torch.randn(B, c.H, device=dev)
+    x16 = x.to(torch.bfloat16) if eng.wdt == torch.bfloat16 else None
+
+    def run():
+        for i, L in enumerate(c.layers):
+            Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18,
+                                 L.o, x, const_pos=pos, x16=x16)
+    us = _graph_us(run, dev, reps) / len(c.layers)
+    L0 = c.layers[0]
+    byt = (L0.o.w.numel() * L0.o.w.element_size() + B * c.Hkv * (pos + 1) * c.D * 2 * kc[0].element_size()
+           + B * c.qkv_w * 4 + B * c.H * (4 + 4 + (2 if x16 is not None else 0)))
+    return dict(name="cp_attn_oproj", kernel=f"attn_oproj_k (code-predictor attention + o_proj + residual, {pos + 1} "
+                                              "keys)", bound="hbm", launches_per_frame=5 * (eng.G - 2), avg_us=us,
+                bytes=byt)
 
 
-def _graph_us(run, dev, reps=10):
-    """Capture run() into a HIP graph on a side stream, replay it `reps` times between HIP events recorded on that
-    stream; returns microseconds per replay (the per-launch dispatch gaps of the graph included)."""
-    st = torch.cuda.Stream(device=dev)
-    st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        run()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            run()
-        g.replay()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            g.replay()
-        e1.record(st)
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1e3 / reps
+def decode_kernel_table(tts, B, L_mean):
+    """Every decode kernel of a frame timed live at its production shape (B rows, bf16): per-launch time x launches per
+    frame gives each kernel's share of the frame; `roofline` in the JSON line is the entry with the largest share.
+    Launch counts per frame: talker 28 layers; code predictor 5 layers x (the 2-token prefill + 14 decode steps), its
+    layer-0 q/k/v of the decode steps comes from the sampler's table gather (bf16 mode)."""
+    from qwen_tts import _hip
+    eng = tts.model.engine
+    t, c, dev = eng.talker, eng.cp, eng.dev
+    bf = torch.bfloat16
+    G = eng.G
+    n_cp = G - 1  # CP forwards per frame: the 2-token prefill + 14 decode steps
+    tab = [
+        _gemv_entry("talker_gateup", "gemv_wt (talker MLP gate/up + SwiGLU, RMS folded)", t.n_layers,
+                    [L.gu for L in t.layers], B, t.H, 2 * t.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
+        _gemv_entry("talker_down", "gemv_wt (talker MLP down + residual)", t.n_layers, [L.down for L in t.layers], B,
+                    t.I, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
+        _gemv_entry("talker_qkv", "gemv_wt (talker q/k/v, RMS folded)", t.n_layers, [L.qkv for L in t.layers], B, t.H,
+                    t.qkv_w, bf, torch.float32, dev, rms=True),
+        _gemv_entry("talker_o", "gemv_wt (talker o_proj + residual)", t.n_layers, [L.o for L in t.layers], B,
+                    t.Hq * t.D, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
+        _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * n_cp,
+                    [L.gu for L in c.layers], B, c.H, 2 * c.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
+        _gemv_entry("cp_down", "gemv_wt (code-predictor down + residual)", c.n_layers * n_cp, [L.down for L in c.layers],
+                    B, c.I, c.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
+        _gemv_entry("cp_qkv", "gemv_wt (code-predictor q/k/v, layers 1-4 of decode steps + prefill)",
+                    (c.n_layers - 1) * (n_cp - 1) + c.n_layers, [L.qkv for L in c.layers], B, c.H, c.qkv_w, bf,
+                    torch.float32, dev, rms=True),
+        _gemv_entry("cp_lm_head", "gemv_wt (code-predictor lm_head, final norm folded)", n_cp, eng.lm_heads, B, c.H,
+                    eng.Vc, bf, torch.float32, dev, rms=True),
+        attn_oproj_entry(tts, B),
+    ]
+    ra = attention_roofline(tts, B, L_mean)
+    tab.append(dict(name="talker_attention", kernel=f"attn_decode_k (talker decode attention, {L_mean} keys)",
+                    bound="hbm", launches_per_frame=t.n_layers, avg_us=ra["avg_us"], bytes=ra["bytes"]))
+    for e in tab:
+        e["gbs"] = e["bytes"] / (e["avg_us"] * 1e-6) / 1e9
+        e["frac"] = e["gbs"] / HBM_PEAK_GBS
+        e["us_per_frame"] = e["avg_us"] * e["launches_per_frame"]
+    return tab
 
 
-def frame_bytes(cfg, B, L_talker):
-    """Algorithmic HBM bytes of one AR frame for B rows at talker cache length L_talker: every
-    talker weight once (28 layers + codec_head), per code-predictor forward (the 2-token prefill + 14 decode steps =
-    15) the 5 layers + that step's lm_head, small_to_mtp once, the talker K/V of every row (28 x 2 x Hkv x D x 2 x L)
-    and the code predictor's K/V (keys 2..16 over the 15 forwards)."""
-    t, c = cfg["talker_config"], cfg["talker_config"]["code_predictor_config"]
+def _pmc_traffic(tag):
+    """HBM traffic per launch of a kernel from the committed rocprofv3 PMC profile (profiles/*_pmc_<tag>.json) whose
+    build id (content digest of the kernel sources) matches this library's; else the newest, labelled as such.
+    Counters cannot be read inside this process."""
+    from qwen_tts import _hip
+    pdir = os.path.join(REPO, "profiles")
+    pmcs = [f for f in sorted(os.listdir(pdir), reverse=True) if f.endswith(f"_pmc_{tag}.json")]
+    for f in pmcs:
+        j = json.load(open(os.path.join(pdir, f)))
+        if j.get("build_id") == _hip.BUILD_ID:
+            return j.get("hbm_bytes_per_launch"), f"profiles/{f} (this build, {j['build_id']})"
+    if pmcs:
+        j = json.load(open(os.path.join(pdir, pmcs[0])))
+        return j.get("hbm_bytes_per_launch"), (f"profiles/{pmcs[0]} (earlier build {j.get('build_id')}, not this "
+                                               f"library's {_hip.BUILD_ID})")
+    return None, None
 
-    def layer_params(d):
-        H, I, hq, hkv, D = d["hidden_size"], d["intermediate_size"], d["num_attention_heads"], d["num_key_value_heads"], \
-            d["head_dim"]
-        return H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I
-    w_t = t["num_hidden_layers"] * layer_params(t) + t["vocab_size"] * t["hidden_size"]
-    w_cp = c["num_hidden_layers"] * layer_params(c) + c["vocab_size"] * c["hidden_size"]
-    s2m = t["hidden_size"] * c["hidden_size"] if t["hidden_size"] != c["hidden_size"] else 0
-    kv_t = t["num_hidden_layers"] * 2 * t["num_key_value_heads"] * t["head_dim"] * 2 * L_talker
-    kv_cp = sum(c["num_hidden_layers"] * 2 * c["num_key_value_heads"] * c["head_dim"] * 2 * j for j in range(2, 17))
-    return 2 * (w_t + 15 * w_cp + s2m) + B * (kv_t + kv_cp)
+
+PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj"}
 
 
 def whole_frame_roofline(tts, cfg, B, reps=32):
@@ -128,30 +191,6 @@ def whole_frame_roofline(tts, cfg, B, reps=32):
     return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, keys=L)
 
 
-def attn_oproj_roofline(tts, B, pos=9, reps=20):
-    """Code-predictor fused attention + o_proj + residual (attn_oproj_k) at cache position `pos` (the mean over the
-    15 steps), 5 launches over the 5 layers' distinct o_proj weights per replay.  Algorithmic bytes per launch =
-    o_proj weights + K/V of (pos + 1) keys + the q/k/v rows read + the residual read and written (fp32 + bf16)."""
-    from qwen_tts import kernels as Kn
-    eng = tts.model.engine
-    c, dev = eng.cp, eng.dev
-    kc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
-    vc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
-    qkv = torch.randn(B, c.qkv_w, device=dev)
-    x = torch.randn(B, c.H, device=dev)
-    x16 = x.to(torch.bfloat16) if eng.wdt == torch.bfloat16 else None
-
-    def run():
-        for i, L in enumerate(c.layers):
-            Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18,
-                                 L.o, x, const_pos=pos, x16=x16)
-    us = _graph_us(run, dev, reps) / len(c.layers)
-    L0 = c.layers[0]
-    byt = (L0.o.w.numel() * L0.o.w.element_size() + B * c.Hkv * (pos + 1) * c.D * 2 * kc[0].element_size()
-           + B * c.qkv_w * 4 + B * c.H * (4 + 4 + (2 if x16 is not None else 0)))
-    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9)
-
-
 def prefill_mfma(tts, M=680, reps=3):
     """Prefill linears on gemm_pf_k at M rows (M = 680: four ~170-token voice-clone prompts, configs[4]): per replay
     the 28 talker layers' q/k/v (RMS), o_proj (+ residual, bf16 shadow), gate/up (RMS, SwiGLU) and down (+ residual)
@@ -175,40 +214,6 @@ def prefill_mfma(tts, M=680, reps=3):
     nk = t.H * t.qkv_w + t.Hq * t.D * t.H + t.H * 2 * t.I + t.I * t.H
     flops = 2.0 * M * nk * len(t.layers)
     return dict(us_per_layer=us / len(t.layers), tflops=flops / (us * 1e-6) / 1e12, M=M)
-
-
-def kernel_roofline(tts, B, reps=10):
-    """Dominant decode kernel timed live: a HIP graph of the 28 production gate-up launches (one per layer,
-    distinct weights, so every launch streams HBM as in a frame), replayed `reps` times between HIP events
-    recorded on the capture stream.  Per-launch time includes the in-graph dispatch gap (conservative)."""
-    from qwen_tts import _hip, kernels as Kn
-    eng = tts.model.engine
-    t = eng.talker
-    dev = eng.dev
-    x = torch.randn(B, t.H, device=dev).to(eng.wdt)  # production A: the bf16 residual shadow (fp32 in fp32 mode)
-    h = torch.empty(B, t.I, dtype=eng.wdt, device=dev)
-
-    def run():
-        for L in t.layers:
-            Kn.gemm(x, L.gu, h, B, t.H, t.I, rms=True, eps=t.eps, epi=_hip.EPI_SWIGLU)
-    st = torch.cuda.Stream(device=dev)
-    st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        run()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            run()
-        g.replay()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            g.replay()
-        e1.record(st)
-    torch.cuda.synchronize()
-    n = reps * len(t.layers)
-    us = e0.elapsed_time(e1) * 1e3 / n
-    byt = gateup_bytes(eng, B)
-    return dict(avg_us=us, bytes=byt, gbs=byt / (us * 1e-6) / 1e9, launches=n)
 
 
 def attention_roofline(tts, B, L, reps=10):
@@ -277,8 +282,10 @@ def cpu_baseline(B, prompt, frames, threads):
         wav = co.decode(codes)
     dt = time.time() - t0
     audio = sum(w.shape[0] for w in wav) / 24000.0
-    return dict(value=audio / dt, unit="audio-seconds/sec", cores=threads, kind="port",
-                sample=f"oracle fp32, 1.7B dims, B={B} x {prompt}-token prompts, {frames} frames + codec, {dt:.1f}s")
+    return dict(value=audio / dt, unit="audio-seconds/sec", cores=threads, threads=threads,
+                host_cpu_count=os.cpu_count(), kind="port",
+                sample=f"oracle fp32, 1.7B dims, B={B} x {prompt}-token prompts, {frames} frames + codec, {dt:.1f}s, "
+                       f"torch.set_num_threads({threads})")
 
 
 def main():
@@ -334,9 +341,9 @@ def main():
                subtalker_dosample=True, subtalker_top_k=50, subtalker_top_p=1.0, subtalker_temperature=0.9,
                repetition_penalty=1.05, ignore_eos=True)
 
-    def step(seed):
+    def step(seed, n=B):
         t0 = time.perf_counter()
-        codes, _ = tts.model.generate(input_ids=ids, languages=langs, speakers=spk, non_streaming_mode=False,
+        codes, _ = tts.model.generate(input_ids=ids[:n], languages=langs[:n], speakers=spk[:n], non_streaming_mode=False,
                                       seed=seed, **gen)
         wavs, sr = tts.model.speech_tokenizer.decode([{"audio_codes": c} for c in codes])
         return sum(w.shape[0] for w in wavs) / sr, time.perf_counter() - t0
@@ -362,11 +369,23 @@ def main():
         from qwen_tts.dp import reduce_timing
         dt, audio = reduce_timing(dt, audio, device=dev)
     value = audio / dt
-    # talker cache length at the end of a timed step (prompt + frames), before stream() reuses the sessions
-    L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine.all_sessions())
+    # talker cache length at the end of a timed step (prompt + frames), before other shapes reuse the sessions
+    L_end = max(int(ss.meta["kv_pos"].max().item()) for ss in tts.model.engine.all_sessions() if ss.B == B)
     fr = whole_frame_roofline(tts, cfg, B) if a.roofline and rank == 0 else None
-    # first packet (SURVEY §8 metric): request submit -> first PCM chunk delivered by stream(), p50 of 3 after a
-    # warmup, on this rank's batch of B and on a single utterance
+    # batch 1 (the metric's "1.7B @ batch 1"): one utterance of the same shape per GPU, 1 warm-up + `steps` timed
+    b1 = None
+    if rank == 0 and B > 1:
+        step(200, 1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        au1 = sum(step(300 + i, 1)[0] for i in range(a.steps))
+        torch.cuda.synchronize()
+        d1 = time.perf_counter() - t1
+        b1 = {"value": round(au1 / d1, 3), "unit": "audio-seconds/sec", "rtf": round(au1 / d1, 2),
+              "ms_per_step": round(1e3 * d1 / a.steps, 2),
+              "workload": f"1 utterance x {a.prompt_tokens}-token prompt, {a.frames} frames + codec, 1 GPU"}
+    # first packet (SURVEY §8 metric): request submit -> first PCM chunk delivered by stream(), on this rank's batch
+    # of B and on a single utterance
     def first_packet(n):
         t0 = time.perf_counter()
         for _ in tts.model.stream(input_ids=ids[:n], languages=langs[:n], speakers=spk[:n], non_streaming_mode=False,
@@ -381,54 +400,42 @@ def main():
         first_packet(n)
         first_packet(n)
         fp[n] = 1e3 * float(np.median([first_packet(n) for _ in range(9)]))
-    roof = attn_roof = frame_roof = ao_roof = pf_roof = None
+    roof = table = frame_roof = pf_roof = gateup = None
     from qwen_tts import _hip
-    if a.roofline and rank == 0:
-        r = kernel_roofline(tts, B)
-        # HBM traffic of this kernel from rocprofv3 PMC counters (FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected:
-        # tools/pmc_gateup.py + tools/pmc_reduce.py); counters cannot be read inside this process, so the value comes
-        # from the committed profile whose build id (content digest of the kernel sources) matches this library's
-        traffic, tsrc = None, None
-        pdir = os.path.join(REPO, "profiles")
-        pmcs = [f for f in sorted(os.listdir(pdir), reverse=True) if f.endswith("_pmc_gateup.json")]
-        for f in pmcs:
-            j = json.load(open(os.path.join(pdir, f)))
-            if j.get("build_id") == _hip.BUILD_ID:
-                traffic, tsrc = j.get("hbm_bytes_per_launch"), f"profiles/{f} (this build, {j['build_id']})"
-                break
-        if tsrc is None and pmcs:  # newest profile of an earlier build of the kernels: labelled as such
-            j = json.load(open(os.path.join(pdir, pmcs[0])))
-            traffic = j.get("hbm_bytes_per_launch")
-            tsrc = f"profiles/{pmcs[0]} (earlier build {j.get('build_id')}, not this library's {_hip.BUILD_ID})"
-        roof = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": round(r["gbs"], 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(r["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": tsrc, "avg_launch_us": round(r["avg_us"], 2), "bytes_per_launch": int(r["bytes"]),
-                "timed_launches": r["launches"]}
+    if a.roofline and rank == 0 and eng_wdt_bf16(tts):
+        # decode attention at the run's mean cache length (prompt + half the frames)
+        L_mean = max(L_end - a.frames // 2, 1)
+        tab = decode_kernel_table(tts, B, L_mean)
+        frame_us = fr["avg_us"] if fr is not None else None
+
+        def as_roof(e):
+            traffic, tsrc = _pmc_traffic(PMC_TAG[e["name"]]) if e["name"] in PMC_TAG else (None, None)
+            return {"bound": e["bound"], "kernel": e["kernel"], "achieved": round(e["gbs"], 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(e["frac"], 4), "traffic": traffic, "traffic_source": tsrc,
+                    "avg_launch_us": round(e["avg_us"], 2), "bytes_per_launch": int(e["bytes"]),
+                    "launches_per_frame": e["launches_per_frame"], "us_per_frame": round(e["us_per_frame"], 1),
+                    "frame_share": None if frame_us is None else round(e["us_per_frame"] / frame_us, 4)}
+        # the dominant decode kernel = the largest measured time per frame (launch time x launches per frame)
+        dom = max(tab, key=lambda e: e["us_per_frame"])
+        roof = dict(as_roof(dom), selected_by="largest measured time per frame among the decode kernels (kernel_table)")
+        gateup = as_roof(next(e for e in tab if e["name"] == "talker_gateup"))
+        table = {e["name"]: {"avg_launch_us": round(e["avg_us"], 2), "launches_per_frame": e["launches_per_frame"],
+                             "us_per_frame": round(e["us_per_frame"], 1), "bytes_per_launch": int(e["bytes"]),
+                             "frac": round(e["frac"], 4)} for e in tab}
         if fr is not None:
             frame_roof = {"bound": "hbm", "what": f"whole AR frame (15 CP steps + talker step), B={B}, "
                                                   f"{fr['keys']} talker keys, captured frame graph replayed",
                           "achieved": round(fr["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(fr["gbs"] / HBM_PEAK_GBS, 4), "us_per_frame": round(fr["avg_us"], 1),
-                          "bytes_per_frame": int(fr["bytes"])}
-        ao = attn_oproj_roofline(tts, B)
-        ao_roof = {"bound": "hbm", "kernel": f"attn_oproj_k (code-predictor attention + o_proj + residual, B={B}, "
-                                             "10 keys)", "achieved": round(ao["gbs"], 1), "peak": HBM_PEAK_GBS,
-                   "unit": "GB/s", "frac": round(ao["gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(ao["avg_us"], 2),
-                   "bytes_per_launch": int(ao["bytes"])}
-        if eng_wdt_bf16(tts):
-            pf = prefill_mfma(tts)
-            pf_roof = {"bound": "mfma", "kernel": f"gemm_pf_k (talker prefill linears, M={pf['M']} rows, 28 layers)",
-                       "achieved": round(pf["tflops"], 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
-                       "frac": round(pf["tflops"] / MFMA_BF16_PEAK_TFS, 4), "us_per_layer": round(pf["us_per_layer"], 1)}
-        # decode attention at the run's mean cache length (prompt + half the frames)
-        L_mean = max(L_end - a.frames // 2, 1)
-        ra = attention_roofline(tts, B, L_mean)
-        attn_roof = {"bound": "hbm", "kernel": f"attn_decode_k (talker decode attention, B={B}, {L_mean} keys)",
-                     "achieved": round(ra["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ra["gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(ra["avg_us"], 2),
-                     "bytes_per_launch": int(ra["bytes"])}
+                          "bytes_per_frame": int(fr["bytes"]),
+                          "kernel_table_us": round(sum(e["us_per_frame"] for e in tab), 1)}
+        pf = prefill_mfma(tts)
+        pf_roof = {"bound": "mfma", "kernel": f"gemm_pf2_k (talker prefill linears, M={pf['M']} rows, 28 layers)",
+                   "achieved": round(pf["tflops"], 1), "peak": MFMA_BF16_PEAK_TFS, "unit": "TFLOP/s",
+                   "frac": round(pf["tflops"] / MFMA_BF16_PEAK_TFS, 4), "us_per_layer": round(pf["us_per_layer"], 1)}
     cpu = None
     if a.cpu_baseline and rank == 0 and world == 1:
+        # the box's CPU share (OMP_NUM_THREADS = 16 there); os.cpu_count() reports the whole host
         cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, int(os.environ.get("OMP_NUM_THREADS", "16")))
     if rank == 0:
         per_utt_rtf = value / (B * world)
@@ -440,12 +447,11 @@ def main():
                                       f"streaming text, {a.frames} frames + codec decode",
                           "global_batch": B * world, "seq_len": a.prompt_tokens, "frames": a.frames,
                           "parallelism": f"dp{world}"},
-               "rtf_per_utterance": round(per_utt_rtf, 2),
+               "rtf_per_utterance": round(per_utt_rtf, 2), "batch1": b1,
                "first_packet_p50_ms": round(fp[B], 1), "first_packet_p50_ms_b1": round(fp[1], 1),
                "full_batch_latency_p50_ms": round(1e3 * float(np.median(lat)), 1),
-               "roofline": roof, "decode_attention_roofline": attn_roof, "frame_roofline": frame_roof,
-               "attn_oproj_roofline": ao_roof, "prefill_mfma": pf_roof, "cpu_baseline": cpu,
-               "build_id": _hip.BUILD_ID}
+               "roofline": roof, "frame_roofline": frame_roof, "kernel_table": table, "gateup_roofline": gateup,
+               "prefill_mfma": pf_roof, "cpu_baseline": cpu, "build_id": _hip.BUILD_ID}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -921,6 +921,297 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
   }
 }
 
+// Head-split form of the fused code-predictor attention + o_proj (header: qt_attn_oproj_args.ws).  Block = (column
+// group cg of NC = 32 o_proj columns, kv head h), linear id h * CG + cg: with CG % 8 == 0 the 8 head blocks of one
+// column group are dealt to one XCD under round-robin placement (speed only, never correctness).  Wave w = row w:
+// q/k RMSNorm + RoPE of head h's NREP + 2 vectors (one per lane group), attention over the row's cached keys + the
+// new key, the NREP x D output into row w of the block's LDS A tile.  Then head h's K-slice of o_proj for the 32
+// columns and every row (NT x KTS MFMA fragments spread over the 8 waves, reduced in LDS in a fixed order).  Row r's
+// partial goes to the block of head r as 32 {value, sequence tag} granules (8-byte agent-scope stores: write-through);
+// that block polls the other heads' granules of its row, sums the nk partials in head order, adds the residual and
+// stores the row (fp32 + the bf16 shadow).  Per-block intake: 16 KiB of weights + head h's K/V of every row + 4
+// vectors per row, against the (column group, row) form's 128 KiB of weights + every head's K/V of one row (that form
+// is bound by the CU's load intake).
+// Sequence tags: granule (cg, p, r, c) carries the number of its producer's publications (the producer reads its own
+// previous tag at kernel start); the consumer keeps its own count C[cg][r] and waits for C + 1.  Nothing is reset, so
+// a write that arrives after a consumer gave up (bounded spin; sticky error flag ws[0]) is never taken for the next
+// launch's.  Cache appends of the new k/v are issued last, after every counted load wait.
+struct AOHS {
+  qt_attn_oproj_args a;
+  int spin_limit;
+};
+
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+QT_DEV size_t aohs_gran_off(int CG, int nk) { return 256 + ((size_t)CG * nk * 4 + 255) / 256 * 256; }
+
+template <int D, int NREP>
+__global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
+  const qt_attn_oproj_args& p = pk.a;
+  constexpr int NW = 8, NT = 2, E = 8, KT = 32, NC = NT * 16;
+  constexpr int KS = NREP * D, KTS = KS / KT, FPW = NT * KTS / NW, WPT = KTS / FPW;  // waves per column tile
+  constexpr int LPK = D / 8, GPW = 64 / LPK, IC = 4;
+  static_assert(FPW >= 1 && KTS % FPW == 0 && GPW >= NREP + 2, "head-split attn_oproj shape");
+  constexpr int ALD = KS + 8;  // bf16 A-tile row stride (16 B pad)
+  __shared__ float qs[NW][NREP][D];
+  __shared__ float kn[NW][D], vn[NW][D];
+  __shared__ __attribute__((aligned(16))) bf16_t att[NW][ALD];
+  __shared__ float red[NW][64][4];
+  __shared__ float part[NW][NC];
+  __shared__ float gath[8][NC];
+  __shared__ int fail_sh;
+  const int R = p.R, nq = p.Hq, nk = p.Hkv;
+  const int CG = gridDim.x / nk;
+  const int h = blockIdx.x / CG, cg = blockIdx.x % CG;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lm = lane & 15, lk = lane >> 4;
+  const int grp = lane / LPK, sub = lane % LPK;
+  const int r = min(w, R - 1);  // this wave's row (waves past R repeat row R - 1 and publish nothing)
+  const int kvpos = p.const_pos, nc = kvpos;  // cached keys [0, kvpos); the new key (kvpos) comes from LDS
+  const int nvec = nq + 2 * nk, half = D / 2;
+  const int e0 = sub * 8, ec = e0 % half;
+  const int vsel = min(grp, NREP + 1);  // lane group -> q head h*NREP + grp, k head h, v head h
+  const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? nq + h : nq + nk + h);
+  const float* xsrc = p.qkv + (long long)r * nvec * D + (long long)hh * D + e0;
+  unsigned* cnt = (unsigned*)((char*)p.ws + 256);
+  unsigned long long* gran = (unsigned long long*)((char*)p.ws + aohs_gran_off(CG, nk));
+  const int ktiles = nq * D / KT;
+
+  // 1. every load, in the order the phases need them (inline asm, counted waits -- see attn_oproj_k)
+  u32x4_t xq[2], nwr[2], cvr[2], svr[2];
+  {
+    const float* nwp = vsel < NREP ? (p.q_norm ? p.q_norm + e0 : xsrc) : (p.k_norm ? p.k_norm + e0 : xsrc);
+    const float* cs = p.cos_tab + (long long)kvpos * half + ec;
+    const float* sn = p.sin_tab + (long long)kvpos * half + ec;
+    asm_ld16(xq[0], xsrc); asm_ld16(xq[1], xsrc + 4);
+    asm_ld16(nwr[0], nwp); asm_ld16(nwr[1], nwp + 4);
+    asm_ld16(cvr[0], cs); asm_ld16(cvr[1], cs + 4);
+    asm_ld16(svr[0], sn); asm_ld16(svr[1], sn + 4);
+  }
+  const long long kvbase = ((long long)r * nk + h) * p.Lmax * D;
+  u32x4_t kq[IC], vq[IC];
+  auto kv_addr = [&](int j0, int c, bool isv) {
+    const int jj = min(j0 + c * GPW + grp, max(nc - 1, 0));  // clamped (masked in the math)
+    return (const bf16_t*)(isv ? p.v_cache : p.k_cache) + kvbase + (long long)jj * D + sub * 8;
+  };
+#pragma unroll
+  for (int c = 0; c < IC; ++c) { asm_ld16(kq[c], kv_addr(0, c, false)); asm_ld16(vq[c], kv_addr(0, c, true)); }
+  const int f0 = w * FPW, tw = f0 / KTS, kt0 = f0 % KTS;
+  u32x4_t wv[FPW];
+  {
+    const bf16_t* wp = (const bf16_t*)p.w_o + ((size_t)(cg * NT + tw) * ktiles + (size_t)h * KTS + kt0) * 64 * E +
+                       lane * E;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) asm_ld16(wv[i], wp + (size_t)i * 64 * E);
+  }
+  // the granule this lane publishes (row w, column lane & 31): its previous tag
+  const size_t my_g = ((size_t)(cg * nk + h) * 8 + w) * NC + (lane & (NC - 1));
+  u32x2_t gprev;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(gprev) : "v"(gran + my_g) : "memory");
+  // residual of the row this block finalises (row h) at this lane's column; this block's consumed count
+  unsigned xres_u, cprev;
+  asm_ld4(xres_u, p.x + (long long)min(h, R - 1) * p.ldx + cg * NC + (lane & (NC - 1)));
+  asm_ld4(cprev, cnt + cg * nk + h);
+  constexpr int N_X = 2, N_T = 1, N_W = FPW, N_KV = 2 * IC;
+
+  // 2. q/k RMSNorm + RoPE of head h's vectors of row r (v passes through), into LDS
+  {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_KV + N_W + N_T + N_X) : "memory");
+    reg_fence(xq[0]); reg_fence(xq[1]); reg_fence(nwr[0]); reg_fence(nwr[1]);
+    reg_fence(cvr[0]); reg_fence(cvr[1]); reg_fence(svr[0]); reg_fence(svr[1]);
+    const bool lo = e0 < half;
+    float nwv[8], cv[8], sv[8], xv[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      nwv[i] = __uint_as_float(nwr[0][i]); nwv[i + 4] = __uint_as_float(nwr[1][i]);
+      cv[i] = __uint_as_float(cvr[0][i]); cv[i + 4] = __uint_as_float(cvr[1][i]);
+      sv[i] = __uint_as_float(svr[0][i]); sv[i + 4] = __uint_as_float(svr[1][i]);
+      xv[i] = __uint_as_float(xq[0][i]); xv[i + 4] = __uint_as_float(xq[1][i]);
+    }
+    if (vsel <= NREP) {
+      const bool isq = vsel < NREP;
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += xv[i] * xv[i];
+      ss = group_sum_dpp<LPK>(ss);
+      const float rs = rsqrtf(ss / (float)D + p.eps);
+      if (isq ? p.q_norm != nullptr : p.k_norm != nullptr) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] = nwv[i] * (xv[i] * rs);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // q*cos + rotate_half(q)*sin
+        const float pt = half_partner<LPK>(xv[i]);
+        xv[i] = lo ? xv[i] * cv[i] - pt * sv[i] : xv[i] * cv[i] + pt * sv[i];
+      }
+    }
+    if (grp < NREP) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qs[w][grp][e0 + i] = xv[i];
+    } else if (grp < NREP + 2) {  // as the cache holds them (bf16 rounding)
+      float* dst = grp == NREP ? kn[w] : vn[w];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dst[e0 + i] = bf2f(f2bf(xv[i]));
+    }
+  }
+  __syncthreads();
+  // 3. attention of (row r, head h): lane group grp owns cached keys grp, grp + GPW, ...; the new key is folded into
+  // lane group 0's state; groups merge through a common max + plain sums
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_W + N_T + N_X) : "memory");
+#pragma unroll
+  for (int c = 0; c < IC; ++c) { reg_fence(kq[c]); reg_fence(vq[c]); }
+  {
+    const float scale = rsqrtf((float)D) * 1.4426950408889634f;  // scores in log2 units (exp2 softmax)
+    float q[NREP][8], m[NREP], l[NREP], o[NREP][8];
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      m[j] = -INFINITY; l[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { q[j][i] = qs[w][j][sub * 8 + i] * scale; o[j][i] = 0.f; }
+    }
+    {  // one batch: the host routes <= GPW * IC cached keys here (no loop, so no compiler wait at a loop preheader)
+      float vf[IC][8], dd[NREP][IC];
+#pragma unroll
+      for (int c = 0; c < IC; ++c) {
+        const int jj = c * GPW + grp;
+        float kf[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          kf[2 * i] = __uint_as_float(kq[c][i] << 16); kf[2 * i + 1] = __uint_as_float(kq[c][i] & 0xFFFF0000u);
+          vf[c][2 * i] = __uint_as_float(vq[c][i] << 16); vf[c][2 * i + 1] = __uint_as_float(vq[c][i] & 0xFFFF0000u);
+        }
+        if (jj >= nc) {  // masked key: weight exactly 0, keep 0 * v finite
+#pragma unroll
+          for (int i = 0; i < 8; ++i) vf[c][i] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < NREP; ++j) {
+          float d = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
+          d = group_sum_dpp<LPK>(d);
+          dd[j][c] = jj < nc ? d : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        float mn = m[j];
+#pragma unroll
+        for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
+        if (mn == -INFINITY) continue;
+        const float f = exp2_hw(m[j] - mn);
+        float e[IC], es = 0.f;
+#pragma unroll
+        for (int c = 0; c < IC; ++c) { e[c] = exp2_hw(dd[j][c] - mn); es += e[c]; }
+        l[j] = l[j] * f + es;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float acc = o[j][i] * f;
+#pragma unroll
+          for (int c = 0; c < IC; ++c) acc += e[c] * vf[c][i];
+          o[j][i] = acc;
+        }
+        m[j] = mn;
+      }
+    }
+    {  // the new key (LDS), lane group 0
+      float kf[8], vv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { kf[i] = kn[w][sub * 8 + i]; vv[i] = vn[w][sub * 8 + i]; }
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
+        d = group_sum_dpp<LPK>(d);
+        if (grp == 0) {
+          const float mn = fmaxf(m[j], d);
+          const float f = exp2_hw(m[j] - mn), e = exp2_hw(d - mn);
+          l[j] = l[j] * f + e;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vv[i];
+          m[j] = mn;
+        }
+      }
+    }
+    GroupMerge<LPK, NREP> gm;
+    gm.run(m, l, o);
+    gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = f2bf(ov / lv); });
+  }
+  __syncthreads();
+  // 4. head h's K-slice of o_proj for the block's 32 columns: wave w multiplies fragments f0 .. f0 + FPW - 1 (column
+  // tile tw); MFMA rows = batch rows (rows >= NW zero)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_T + N_X) : "memory");
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) reg_fence(wv[i]);
+  {
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      u32x4_t av = {0u, 0u, 0u, 0u};
+      if (lm < NW) av = *(const u32x4_t*)&att[lm][(kt0 + i) * KT + lk * E];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av), __builtin_bit_cast(bf16x8_t, wv[i]),
+                                                    acc, 0, 0, 0);
+    }
+    red[w][lane][0] = acc[0]; red[w][lane][1] = acc[1]; red[w][lane][2] = acc[2]; red[w][lane][3] = acc[3];
+  }
+  if (tid == 0) fail_sh = 0;
+  __syncthreads();
+  // 5. row w's partial (thread (w, c < NC)): the column tile's waves summed in wave order; publish it to the block of
+  // head w (rows < R other than h), keep row h
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_X) : "memory");
+  reg_fence(gprev);
+  if (lane < NC) {
+    const int c = lane, t = c >> 4, cc = c & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int q2 = 0; q2 < WPT; ++q2) v += red[t * WPT + q2][(w >> 2) * 16 + cc][w & 3];
+    part[w][c] = v;
+    if (w < R && w != h)
+      __hip_atomic_store(gran + my_g, ((unsigned long long)(gprev[1] + 1u) << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 6. block of head h < R: the other heads' partials of row h, then the row
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  reg_fence(xres_u); reg_fence(cprev);
+  if (h < R) {
+    const unsigned want = cprev + 1u;
+    if (tid < (nk - 1) * NC) {
+      const int pi = tid / NC, c = tid % NC, pp = pi < h ? pi : pi + 1;
+      const unsigned long long* src = gran + ((size_t)(cg * nk + pp) * 8 + h) * NC + c;
+      unsigned long long g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int spins = 0;
+      while ((unsigned)(g >> 32) != want) {
+        if (++spins > pk.spin_limit) { fail_sh = 1; break; }
+        __builtin_amdgcn_s_sleep(1);
+        g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      gath[pp][c] = __uint_as_float((unsigned)g);
+    }
+    __syncthreads();
+    if (tid < NC) {
+      float v = 0.f;
+      for (int pp = 0; pp < nk; ++pp) v += pp == h ? part[h][tid] : gath[pp][tid];
+      const float y = __uint_as_float(xres_u) + v;
+      const int col = cg * NC + tid;
+      p.x[(long long)h * p.ldx + col] = y;
+      if (p.x16) ((bf16_t*)p.x16)[(long long)h * p.ldx16 + col] = f2bf(y);
+    }
+    if (tid == 0) {
+      cnt[cg * nk + h] = want;
+      if (fail_sh) atomicOr((int*)p.ws, 1);
+    }
+  }
+  // 7. the new k / v of (row w, head h) into the caches (one column group appends)
+  if (cg == 0 && w < R && lane < D) {
+    const long long o = (((long long)w * nk + h) * p.Lmax + kvpos) * D + lane;
+    ((bf16_t*)p.k_cache)[o] = f2bf(kn[w][lane]);
+    if (lane + 64 < D) ((bf16_t*)p.k_cache)[o + 64] = f2bf(kn[w][lane + 64]);
+    ((bf16_t*)p.v_cache)[o] = f2bf(vn[w][lane]);
+    if (lane + 64 < D) ((bf16_t*)p.v_cache)[o + 64] = f2bf(vn[w][lane + 64]);
+  }
+}
+
 template <typename WT, int D, int NREP, bool CPOS>
 int attn_oproj_go(const qt_attn_oproj_args& a, hipStream_t s) {
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
@@ -1025,6 +1316,11 @@ extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
   }
 }
 
+extern "C" long long qt_attn_oproj_ws_bytes(int N, int Hkv) {
+  const long long cg = (N + 31) / 32;
+  return 256 + (cg * Hkv * 4 + 255) / 256 * 256 + cg * Hkv * 8 * 32 * 8;
+}
+
 extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   if (!a || a->R <= 0 || a->Hkv <= 0 || a->Hkv > 8 || a->Hq % a->Hkv || a->N <= 0 || a->Lmax <= 0) return QT_ERR_SHAPE;
   if (!a->qkv || !a->w_o || !a->x || !a->k_cache || !a->v_cache || !a->cos_tab || !a->sin_tab) return QT_ERR_ARG;
@@ -1032,6 +1328,15 @@ extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   if (a->w_dtype != a->kv_dtype || (a->w_dtype != QT_BF16 && a->w_dtype != QT_F32)) return QT_ERR_DTYPE;
   hipStream_t s = (hipStream_t)stream;
   const bool bf = a->w_dtype == QT_BF16;
+  // head-split form (a workspace was given and the shape is the code predictor's): QT_AO_HS=0 keeps the (column
+  // group, row) form (A/B); QT_AO_SPIN bounds each hand-off poll (iterations of ~1 us)
+  static const int hs_env = [] { const char* e = getenv("QT_AO_HS"); return e ? atoi(e) : 1; }();
+  static const int spin = [] { const char* e = getenv("QT_AO_SPIN"); return e ? atoi(e) : 200000; }();
+  if (hs_env && a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
+      a->R <= 8 && a->N % 256 == 0 && a->const_pos < a->Lmax && a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv)) {
+    hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(a->N / 32 * a->Hkv), dim3(512), 0, s, AOHS{*a, spin});
+    return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+  }
   switch (a->D) {
     case 16: return bf ? attn_oproj_rep<bf16_t, 16>(*a, s) : attn_oproj_rep<float, 16>(*a, s);
     case 64: return bf ? attn_oproj_rep<bf16_t, 64>(*a, s) : attn_oproj_rep<float, 64>(*a, s);

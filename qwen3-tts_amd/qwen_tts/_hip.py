@@ -66,7 +66,8 @@ class AttnOprojArgs(ctypes.Structure):
                 ("q_norm", c_void_p), ("k_norm", c_void_p), ("eps", c_float), ("cos_tab", c_void_p), ("sin_tab", c_void_p),
                 ("rope_pos", c_void_p), ("kv_pos", c_void_p), ("row_start", c_void_p), ("const_pos", c_int),
                 ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int), ("w_o", c_void_p), ("w_dtype", c_int),
-                ("N", c_int), ("x", c_void_p), ("ldx", c_ll), ("x16", c_void_p), ("ldx16", c_ll)]
+                ("N", c_int), ("x", c_void_p), ("ldx", c_ll), ("x16", c_void_p), ("ldx16", c_ll), ("ws", c_void_p),
+                ("ws_bytes", c_ll)]
 
 
 class SampleArgs(ctypes.Structure):
@@ -86,7 +87,7 @@ class SampleArgs(ctypes.Structure):
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
-           "qt_decode_attn_oproj",
+           "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -143,6 +144,7 @@ def load_library(path: str = LIB_PATH):
         "qt_clamp_pcm": [P, c_int, c_ll, P, P],
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
         "qt_decode_attn_oproj": [P, P],
+        "qt_attn_oproj_ws_bytes": [c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],

@@ -254,10 +254,15 @@ def decode_attention(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, rope_pos
     check(_hip.lib().qt_decode_attention(ctypes.byref(a), stream()), "qt_decode_attention")
 
 
+def attn_oproj_ws_bytes(N, Hkv):
+    return int(_hip.lib().qt_attn_oproj_ws_bytes(N, Hkv))
+
+
 def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc, Lmax, w_o: "Tiled", x, *,
-                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None, x16=None):
+                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None, x16=None, ws=None):
     """qt_decode_attn_oproj: x[:R] += o_proj(decode attention) in one launch (row r = batch entry r, short caches).
-    x16: bf16 shadow of x, updated alongside."""
+    x16: bf16 shadow of x, updated alongside.  ws: zeroed uint8 scratch of attn_oproj_ws_bytes(N, Hkv), private to
+    one stream -- enables the head-split form (its int32 word 0 is the sticky hand-off error flag)."""
     a = _hip.AttnOprojArgs()
     a.R, a.Hq, a.Hkv, a.D, a.Lmax = R, Hq, Hkv, D, Lmax
     a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
@@ -268,6 +273,8 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
     a.x, a.ldx = ptr(x), x.stride(0)
     if x16 is not None:
         a.x16, a.ldx16 = ptr(x16), x16.stride(0)
+    if ws is not None:
+        a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
     check(_hip.lib().qt_decode_attn_oproj(ctypes.byref(a), stream()), "qt_decode_attn_oproj")
 
 

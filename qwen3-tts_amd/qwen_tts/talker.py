@@ -97,11 +97,14 @@ class _Stack:
                 K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
-                                    self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"], x16=x16)
+                                    self.cos, self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"], x16=x16,
+                                    ws=scratch.get("ao_ws"))
             elif decode:
+                ns = meta.get("nsplit", 1)
                 K.decode_attention(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
                                    self.cos, self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"],
-                                   meta["row_start"], kc, vc, Lmax, scratch["att"], const_pos=meta.get("const_pos", -1))
+                                   meta["row_start"], kc, vc, Lmax, scratch["att"], const_pos=meta.get("const_pos", -1),
+                                   nsplit=ns, ws=scratch.get("attn_ws") if ns > 1 else None)
             elif "small_T" in meta:  # every key is new and rows are [batch][token]: one fused launch
                 K.small_prefill_attention(scratch["qkv"], R, meta["small_T"], self.Hq, self.Hkv, self.D, L.q_norm,
                                           L.k_norm, self.eps, self.cos, self.sin, kc, vc, Lmax, scratch["att"])
@@ -139,6 +142,19 @@ PF = _hip.env_int("QT_PF", 1) != 0  # parsed as the library parses it (C atoi)
 PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
 # the generation config's min_new_tokens (M:2044-2066): EOS is suppressed while a row has generated fewer tokens
 MIN_NEW_TOKENS = 2
+# talker decode attention split-KV by cache length: (keys below which, nsplit) -- one (row, kv head) block streams
+# ~40 GB/s, so long caches need more blocks; the frame graph is captured once per split factor and the host picks the
+# graph from its bound on the longest row's key count (tools/talker_attn_bench.py, profiles/r04_attn_long.txt).
+# QT_ATTN_SPLIT=0 keeps one block per (row, kv head) at every length (A/B)
+ATTN_SPLIT = [(448, 1), (1024, 2), (2048, 4), (1 << 30, 8)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
+
+
+def attn_nsplit(keys: int) -> int:
+    """Split factor of the talker decode attention for rows of at most `keys` cached keys."""
+    for lim, ns in ATTN_SPLIT:
+        if keys < lim:
+            return ns
+    return ATTN_SPLIT[-1][1]
 
 
 def _lru_get(d: OrderedDict, key):
@@ -164,7 +180,19 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
     sc = {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
     sc["attn_oproj"] = attn_oproj and ATTN_OPROJ and _attn_oproj_ok(st)
+    if sc["attn_oproj"]:  # hand-off granules + sequence counters of the head-split fused kernel (zeroed once)
+        sc["ao_ws"] = torch.zeros(K.attn_oproj_ws_bytes(st.H, st.Hkv), dtype=torch.uint8, device=dev)
     return sc
+
+
+def check_handoffs(sessions):
+    """Raise if a head-split attention + o_proj launch of these sessions gave up waiting for a hand-off (the sticky
+    flag in its workspace): its output rows would hold stale partial sums.  Reads a device word (host sync)."""
+    for s in sessions:
+        ws = s.cp.sc.get("ao_ws")
+        if ws is not None and int(ws[:4].view(torch.int32).item()) != 0:
+            raise RuntimeError("qt_decode_attn_oproj: a head-split hand-off timed out (blocks not co-resident?); "
+                               "outputs of this session are invalid (QT_AO_HS=0 selects the form without hand-offs)")
 
 
 def _attn_oproj_ok(st: _Stack) -> bool:
@@ -271,6 +299,9 @@ class Session:
         self.logits = f32(B, eng.V)
         self.cp_x = f32(2 * B, c.H)
         self.sc_t = _scratch(B, t, dev)
+        # split-KV records + arrival counters of the talker decode attention (zeroed; every launch re-arms them)
+        self.sc_t["attn_ws"] = torch.zeros(K.decode_attn_ws_bytes(B, t.Hq, t.Hkv, t.D, 8), dtype=torch.uint8,
+                                           device=dev)
         self.codes = i32(B, max_frames + 2, self.G)
         # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
         self.force = i32(B, max_frames + 2, self.G) if teacher else None
@@ -284,7 +315,8 @@ class Session:
         self.pad_embed = f32(t.H)
         self.ws = K.new_workspace(dev)  # split-K scratch private to this session's stream
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox key, read by the captured samplers
-        self.graph = None
+        self.graph = None   # the frame graph of the current split factor (graphs[nsplit])
+        self.graphs = {}    # talker attention split factor -> captured frame graph
         # prompt length P -> static prefill buffers (+ captured graph once P repeats); LRU, PREFILL_CACHE lengths
         self.prefill = OrderedDict()
         self.slot_prefill = OrderedDict()  # P -> static single-request prefill buffers (serve() refills); LRU
@@ -527,15 +559,10 @@ class TalkerEngine:
                 s.force[b, :c.shape[0]] = torch.as_tensor(c).to(self.dev, torch.int32)
             with K.use_workspace(s.ws):
                 self._prefill(s, embeds, mask, trailing, tts_pad, gp.resolve_seed())
-                if use_graph and s.graph is None:
-                    s.graph = self._capture(s)
             s.hiddens[:, 0].copy_(s.past_hidden)
-            for _ in range(F):
-                if use_graph:
-                    s.graph.replay()
-                else:
-                    with K.use_workspace(s.ws):
-                        self._frame(s)
+            for f in range(F):
+                self._run_frame(s, P + f + 1, use_graph)
+            check_handoffs([s])
             return s.pick[:, :F].long().cpu(), s.hiddens[:, :F].cpu()
         finally:
             self.release([s])
@@ -557,8 +584,6 @@ class TalkerEngine:
             sessions.append(s)
             with K.use_workspace(s.ws):
                 self._prefill(s, embeds, mask, trailing, tts_pad, seed, philox_ids)
-                if max_frames > 0 and use_graph and s.graph is None:
-                    s.graph = self._capture(s)
             yield from self._frames(sessions, [main], max_frames, use_graph, on_frames, every, first, grow)
         finally:
             self.release(sessions)
@@ -578,11 +603,7 @@ class TalkerEngine:
         while frames < max_frames:
             for s, st in zip(sessions, streams):
                 with torch.cuda.stream(st):
-                    if use_graph:
-                        s.graph.replay()
-                    else:
-                        with K.use_workspace(s.ws):
-                            self._frame(s)
+                    self._run_frame(s, s.P + frames + 1, use_graph)  # every row holds <= P + frames + 1 keys
             frames += 1
             if on_frames is not None:
                 on_frames(sessions[0], frames)
@@ -610,6 +631,7 @@ class TalkerEngine:
                     break
         for st in streams:
             main.wait_stream(st)
+        check_handoffs(sessions)
         yield sessions, frames, True
 
     def collect(self, sessions, frames):
@@ -680,16 +702,13 @@ class TalkerEngine:
                 slot_req = list(range(B))
                 epoch = [0] * B
                 start = [0] * B  # host frame count when the slot's request started
-                if use_graph and s.graph is None:
-                    s.graph = self._capture(s)
+                slot_p = [Pb] * B  # prompt length (K/V rows before the first frame) of each slot's request
                 polls, harvests = [], []
                 frame = 0
                 while any(r >= 0 for r in slot_req) or harvests:
                     if any(r >= 0 for r in slot_req):
-                        if use_graph:
-                            s.graph.replay()
-                        else:
-                            self._frame(s)
+                        keys = max(slot_p[b] + frame - start[b] + 1 for b in range(B) if slot_req[b] >= 0)
+                        self._run_frame(s, min(keys, s.Lmax), use_graph)
                         frame += 1
                         if frame % poll == 0 and not gp.ignore_eos:  # (with ignore_eos only frame counts end rows)
                             st = torch.empty(2 * B, dtype=torch.int32, pin_memory=True)
@@ -725,6 +744,7 @@ class TalkerEngine:
                         start[b] = frame
                         slot_req[b] = queue.pop(0) if queue else -1
                         if slot_req[b] >= 0:
+                            slot_p[b] = int(requests[slot_req[b]][0].shape[0])
                             self._prefill_slot(s, b, requests[slot_req[b]], pids[slot_req[b]])
                         else:
                             s.finished[b:b + 1].fill_(1)  # idle slot: emits EOS until the session ends
@@ -736,6 +756,7 @@ class TalkerEngine:
                         hit = (hc[:F + 1, 0] == eos).nonzero()
                         F = int(hit[0]) if hit.numel() else F
                         yield i, hc[:F].long(), hh[:F].clone()
+                check_handoffs([s])
                 self.serve_stats = {"frames": frame, "slots": B, "requests": n}
         finally:
             self.release([s])
@@ -787,6 +808,7 @@ class TalkerEngine:
         B, P, H = embeds.shape
         t = self.talker
         dev = self.dev
+        s.P = P  # padded prompt length: every row's decode keys are <= P + frames + 1
         # reset per-request state
         for z in (s.seen, s.finished, s.codes, s.ctr):
             z.zero_()
@@ -866,6 +888,22 @@ class TalkerEngine:
         s.ctr.copy_(snap[0]); s.seen.copy_(snap[1]); s.finished.copy_(snap[2]); s.codes.copy_(snap[3])
         s.tok0.copy_(snap[4]); s.seed.copy_(snap[5])
         return g
+
+    def _run_frame(self, s: Session, keys: int, use_graph: bool = True):
+        """One frame of session s whose rows hold at most `keys` cached talker keys (a host-side bound): the talker
+        decode attention's split factor follows the length (attn_nsplit); with graphs, the frame graph of that factor
+        is replayed (captured the first time the factor is needed -- a graph binds its launch grids)."""
+        ns = attn_nsplit(keys)
+        s.meta["nsplit"] = ns
+        if not use_graph:
+            with K.use_workspace(s.ws):
+                self._frame(s)
+            return
+        g = s.graphs.get(ns)
+        if g is None:
+            g = s.graphs[ns] = self._capture(s)
+        s.graph = g
+        g.replay()
 
     def _capture(self, s: Session):
         # the graph must not see the prefill-time counter values: it only reads device memory

@@ -564,6 +564,51 @@ def test_decode_attn_oproj_matches_two_kernel_path(D, hq, hkv, L, N, B, dt):
     Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc5, vc5, Lmax, wo, x5,
                          rope_pos=pos, kv_pos=pos, row_start=start)
     torch.testing.assert_close(x5, x4, atol=tol, rtol=tol)
+    # head-split form (a workspace given; bf16, D = 128, Hq = 2 Hkv, <= 8 rows, N % 256 == 0, <= 16 cached keys):
+    # same results within the tolerance, bitwise reproducible over repeated launches on one workspace (the sequence
+    # tags advance), same cache writes, the error flag clear; the x16 shadow = bf16(x)
+    if dt == torch.bfloat16 and D == 128 and hq == 2 * hkv and B <= 8 and N % 256 == 0 and L - 1 <= 16:
+        ws = torch.zeros(Kn.attn_oproj_ws_bytes(N, hkv), dtype=torch.uint8, device=dev)
+        hs = []
+        for _ in range(3):
+            kc6, vc6 = kc.clone(), vc.clone()
+            x6 = x0.clone()
+            x16 = torch.zeros(B, N, dtype=torch.bfloat16, device=dev)
+            Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kc6, vc6, Lmax, wo, x6, const_pos=L - 1,
+                                 x16=x16, ws=ws)
+            assert torch.equal(kc6, kc2) and torch.equal(vc6, vc2)
+            assert torch.equal(x16, x6.to(torch.bfloat16))
+            hs.append(x6)
+        assert torch.equal(hs[0], hs[1]) and torch.equal(hs[0], hs[2])
+        torch.testing.assert_close(hs[0], x1, atol=tol, rtol=tol)
+        assert int(ws[:4].view(torch.int32).item()) == 0
+
+
+def test_attn_oproj_head_split_tags_across_row_counts():
+    """The head-split fused attention + o_proj on ONE workspace across launches with changing row counts (8, 3, 1, 8)
+    and key counts: every launch equals the (column group, row) form within bf16 tolerance and the hand-off sequence
+    tags stay consistent (no stale granule is taken, no poll gives up)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    D, hq, hkv, N = 128, 16, 8, 1024
+    g = torch.Generator().manual_seed(77)
+    Lmax = 18
+    qn, kn = (1 + 0.1 * torch.randn(D, generator=g)).to(dev), (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    wo = Kn.tile_linear((torch.randn(N, hq * D, generator=g) * 0.05).to(dev), torch.bfloat16)
+    cos, sin = Kn.rope_tables(D, 1e6, Lmax + 8, dev)
+    ws = torch.zeros(Kn.attn_oproj_ws_bytes(N, hkv), dtype=torch.uint8, device=dev)
+    for B, pos in ((8, 3), (3, 16), (1, 0), (8, 9), (5, 12), (8, 16)):
+        qkv = torch.randn(B, (hq + 2 * hkv) * D, generator=g).to(dev)
+        kc = torch.randn(B, hkv, Lmax, D, generator=g).to(dev, torch.bfloat16)
+        vc = torch.randn(B, hkv, Lmax, D, generator=g).to(dev, torch.bfloat16)
+        x0 = torch.randn(B, N, generator=g).to(dev)
+        xa, xb = x0.clone(), x0.clone()
+        kca, vca, kcb, vcb = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+        Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kca, vca, Lmax, wo, xa, const_pos=pos)
+        Kn.decode_attn_oproj(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, kcb, vcb, Lmax, wo, xb, const_pos=pos, ws=ws)
+        torch.testing.assert_close(xb, xa, atol=2e-2, rtol=2e-2)
+        assert torch.equal(kca, kcb) and torch.equal(vca, vcb)
+    assert int(ws[:4].view(torch.int32).item()) == 0
 
 
 @pytest.mark.parametrize("D,hq,hkv", [(128, 16, 8), (16, 4, 2), (64, 4, 4)])
@@ -910,6 +955,32 @@ def test_talker_greedy_codes_bit_exact(tiny_models, use_graph):
         for j, c in enumerate(codes):
             np.testing.assert_array_equal(c.numpy(), z[f"{key}/codes{j}"], err_msg=key)
             np.testing.assert_allclose(hid[j].numpy(), z[f"{key}/hidden{j}"], atol=2e-4, rtol=2e-4, err_msg=key)
+
+
+def test_talker_split_kv_by_length_bit_exact(tiny_models, monkeypatch):
+    """The talker decode attention's length-bucketed split-KV (talker.attn_nsplit: one frame graph per split factor,
+    picked by the host's bound on the longest row's keys) with thresholds lowered so every frame of the golden
+    cases runs split 2, 3, 4 or 8 and the graph switches mid-decode: codes equal the reference fixtures bit for
+    bit (fp32), graph and eager."""
+    from cases import talker_cases
+    from qwen_tts import talker as T
+    from qwen_tts.model import TTSModel
+    monkeypatch.setattr(T, "ATTN_SPLIT", [(12, 2), (24, 3), (40, 4), (1 << 30, 8)])
+    z = np.load(os.path.join(GOLD, "tiny_talker.npz"))
+    cases = talker_cases()
+    switched = 0
+    for use_graph in (True, False):
+        for idx, (key, case) in enumerate(cases.items()):
+            if case.get("do_sample") or key.startswith("vd_"):
+                continue
+            cfg, W, _ = tiny_models["tiny-customvoice"]
+            model = TTSModel(cfg, W, dtype="fp32")
+            codes, _ = _run_case(model, key, case, idx, cfg, use_graph)
+            for j, c in enumerate(codes):
+                np.testing.assert_array_equal(c.numpy(), z[f"{key}/codes{j}"], err_msg=key)
+            if use_graph:
+                switched += max(len(s.graphs) for s in model.engine.all_sessions()) >= 2
+    assert switched >= 3  # the split factor changed mid-decode (a second graph captured) in most cases
 
 
 def test_checkpoint_directory_drop_in(tiny_models, tmp_path):

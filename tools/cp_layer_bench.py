@@ -48,18 +48,30 @@ def main():
         i = nxt()
         K.decode_attn_oproj(qkv, B, hq, hkv, D, qn, qn, 1e-6, cos, sin, kc[i], vc[i], L + 1, o_w[i], x,
                             const_pos=L - 1)
+    ws = torch.zeros(K.attn_oproj_ws_bytes(H, hkv), dtype=torch.uint8, device=dev)
+
+    def fused_hs():
+        i = nxt()
+        K.decode_attn_oproj(qkv, B, hq, hkv, D, qn, qn, 1e-6, cos, sin, kc[i], vc[i], L + 1, o_w[i], x,
+                            const_pos=L - 1, ws=ws)
     timed(qkv_gemv, "qkv GEMV 1024->4096 rms")
     timed(attn, "decode attention (17 keys)")
     timed(oproj, "o_proj GEMV 2048->1024 +res")
     timed(fused, "fused attention + o_proj")
+    timed(fused_hs, "fused attention + o_proj, head-split (hand-offs)")
 
     def chain2():
         qkv_gemv(); attn(); oproj()
 
     def chain1():
         qkv_gemv(); fused()
+
+    def chain1h():
+        qkv_gemv(); fused_hs()
     timed(chain2, "chain qkv -> attn -> o_proj (per 3 launches)")
     timed(chain1, "chain qkv -> fused (per 2 launches)")
+    timed(chain1h, "chain qkv -> fused head-split (per 2 launches)")
+    print("hand-off error flag", int(ws[:4].view(torch.int32).item()))
 
 
 if __name__ == "__main__":

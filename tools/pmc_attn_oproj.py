@@ -27,11 +27,13 @@ vc = [torch.randn(B, c.Hkv, 18, c.D, device=dev).to(torch.bfloat16) for _ in c.l
 qkv = torch.randn(B, c.qkv_w, device=dev)
 x = torch.randn(B, c.H, device=dev)
 x16 = x.to(torch.bfloat16)
+ws = torch.zeros(Kn.attn_oproj_ws_bytes(c.H, c.Hkv), dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
-for _ in range(4):
-    for i, L in enumerate(c.layers):
-        Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18, L.o,
-                             x, const_pos=pos, x16=x16)
+for hs in (False, True):  # the (column group, row) form (attn_oproj_k), then the head-split form (attn_oproj_hs_k)
+    for _ in range(4):
+        for i, L in enumerate(c.layers):
+            Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18,
+                                 L.o, x, const_pos=pos, x16=x16, ws=ws if hs else None)
 torch.cuda.synchronize()
 L0 = c.layers[0]
 algo = (L0.o.w.numel() * 2 + B * c.Hkv * (pos + 1) * c.D * 2 * 2 + B * c.qkv_w * 4 + B * c.H * (4 + 4 + 2))

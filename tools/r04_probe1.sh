@@ -12,3 +12,4 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_R
   timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d $d -o run -- python3 tools/pmc_attn_oproj.py > $d.log 2>&1
 done
 python3 tools/pmc_kernel_reduce.py attn_oproj_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04_pmc_attn_oproj.json
+python3 tools/pmc_kernel_reduce.py attn_oproj_hs_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04_pmc_attn_oproj_hs.json
