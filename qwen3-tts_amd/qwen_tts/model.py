@@ -517,8 +517,10 @@ class TTSModel:
             # every row starts with reference frames, known at submit: decode them on a side stream while the talker
             # prefills and generates the first frames on this one
             _, side, cs, fed = self._start_ref_decode(dec, pre, B)
+        # a one-frame first chunk is handed over as soon as frame 0's codes exist: its codec window is queued before the
+        # talker step that starts frame 1 (the first packet does not wait for it)
         it = self.engine.decode_iter(emb, mask, trail, pad, gp, use_graph=use_graph, every=chunk_frames,
-                                     first=first_chunk_frames, grow=True)
+                                     first=first_chunk_frames, grow=True, early_first=first_chunk_frames == 1)
         try:
             for sessions, frames, final in it:
                 if side is not None:

@@ -474,11 +474,15 @@ class TalkerEngine:
                  emb16=None if s.cp_x16 is None else (s.cp_x16.view(-1)[(2 * b0 + 1) * Hc:], 2 * Hc),
                  force=None if s.force is None else s.force[b0:b1], pick=None if s.pick is None else s.pick[b0:b1])
 
-    def _frame(self, s: Session):
-        """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0."""
+    def _frame(self, s: Session, part: str = "all"):
+        """One decode step (M:1669-1744): CP 15 tokens -> 16-codebook embed sum -> talker -> next cb0.  part = "cp"
+        issues only the code predictor (after it the frame's 16 codes are complete), "talk" only the rest."""
         B, t = s.B, self.talker
         codes_ld = s.codes.shape[1] * self.G
-        self._cp_lane(s, s.cp)
+        if part != "talk":
+            self._cp_lane(s, s.cp)
+        if part == "cp":
+            return
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
@@ -568,12 +572,15 @@ class TalkerEngine:
             self.release([s])
 
     def decode_iter(self, embeds, mask, trailing, tts_pad, gp: GenParams, use_graph: bool = True, on_frames=None,
-                    every: int = 0, first: int = 0, grow: bool = False, philox_ids=None):
+                    every: int = 0, first: int = 0, grow: bool = False, philox_ids=None, early_first: bool = False):
         """Prefill + frame loop as a generator: yields (sessions, frames_done, final) after `first` frames, then
         every `every` frames (0: only at the end; grow=True: intervals double from first - 1 up to `every`), and once
         at the end with final=True.  `sessions` is a one-element list (the batch's session); codes[:, :frames_done]
         are final when yielded (device), and codes[:, frames_done, 0] already holds the next frame's cb0 (EOS of rows
-        that just finished)."""
+        that just finished).  early_first (with first == 1): the first yield comes as soon as frame 0's codes are
+        complete -- after its code predictor, before the talker step that starts frame 1 (which is queued after the
+        caller's work, e.g. the first codec window); at that yield codes[:, 1, 0] is not written yet (EOS cannot occur
+        there anyway: it is masked below min_new_tokens)."""
         B, P, H = embeds.shape
         max_frames = max(gp.max_new_tokens - 1, 0)
         seed = gp.resolve_seed()
@@ -584,11 +591,11 @@ class TalkerEngine:
             sessions.append(s)
             with K.use_workspace(s.ws):
                 self._prefill(s, embeds, mask, trailing, tts_pad, seed, philox_ids)
-            yield from self._frames(sessions, [main], max_frames, use_graph, on_frames, every, first, grow)
+            yield from self._frames(sessions, [main], max_frames, use_graph, on_frames, every, first, grow, early_first)
         finally:
             self.release(sessions)
 
-    def _frames(self, sessions, streams, max_frames, use_graph, on_frames, every, first, grow=False):
+    def _frames(self, sessions, streams, max_frames, use_graph, on_frames, every, first, grow=False, early_first=False):
         main = torch.cuda.current_stream(self.dev)
         frames = 0
         check_every = 8
@@ -601,9 +608,10 @@ class TalkerEngine:
         # memory behind an event; the copy from the previous window is read once its event has completed
         pending = []
         while frames < max_frames:
+            early = early_first and frames == 0 and next_yield == 1 and max_frames > 1
             for s, st in zip(sessions, streams):
-                with torch.cuda.stream(st):
-                    self._run_frame(s, s.P + frames + 1, use_graph)  # every row holds <= P + frames + 1 keys
+                with torch.cuda.stream(st):  # every row holds <= P + frames + 1 keys
+                    self._run_frame(s, s.P + frames + 1, use_graph, "cp" if early else "all")
             frames += 1
             if on_frames is not None:
                 on_frames(sessions[0], frames)
@@ -613,6 +621,10 @@ class TalkerEngine:
                 yield sessions, frames, False
                 interval = min(every, 2 * interval) if grow else every
                 next_yield = frames + interval if every else 0
+            if early:  # the rest of frame 0 (talker step -> cb0 of frame 1), behind the caller's work
+                for s, st in zip(sessions, streams):
+                    with torch.cuda.stream(st):
+                        self._run_frame(s, s.P + 1, use_graph, "talk")
             if frames % check_every == 0 and frames < max_frames:
                 flags = []
                 for s, st in zip(sessions, streams):
@@ -889,23 +901,25 @@ class TalkerEngine:
         s.tok0.copy_(snap[4]); s.seed.copy_(snap[5])
         return g
 
-    def _run_frame(self, s: Session, keys: int, use_graph: bool = True):
+    def _run_frame(self, s: Session, keys: int, use_graph: bool = True, part: str = "all"):
         """One frame of session s whose rows hold at most `keys` cached talker keys (a host-side bound): the talker
         decode attention's split factor follows the length (attn_nsplit); with graphs, the frame graph of that factor
-        is replayed (captured the first time the factor is needed -- a graph binds its launch grids)."""
+        is replayed (captured the first time the factor is needed -- a graph binds its launch grids).  part: "all",
+        or "cp" / "talk" for a frame issued in two pieces (_frame)."""
         ns = attn_nsplit(keys)
         s.meta["nsplit"] = ns
         if not use_graph:
             with K.use_workspace(s.ws):
-                self._frame(s)
+                self._frame(s, part)
             return
-        g = s.graphs.get(ns)
+        g = s.graphs.get((ns, part))
         if g is None:
-            g = s.graphs[ns] = self._capture(s)
-        s.graph = g
+            g = s.graphs[(ns, part)] = self._capture(s, part)
+        if part == "all":
+            s.graph = g
         g.replay()
 
-    def _capture(self, s: Session):
+    def _capture(self, s: Session, part: str = "all"):
         # the graph must not see the prefill-time counter values: it only reads device memory
         snap = s.ctr.clone(), s.seen.clone(), s.finished.clone(), s.codes.clone(), s.tok0.clone(), s.seed.clone()
         side = torch.cuda.Stream()
@@ -913,7 +927,7 @@ class TalkerEngine:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side), K.use_workspace(s.ws):
             with torch.cuda.graph(g, stream=side):
-                self._frame(s)
+                self._frame(s, part)
         torch.cuda.current_stream().wait_stream(side)
         # capture does not execute kernels on ROCm/CUDA; restore anyway for safety
         s.ctr.copy_(snap[0]); s.seen.copy_(snap[1]); s.finished.copy_(snap[2]); s.codes.copy_(snap[3])
