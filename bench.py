@@ -53,6 +53,45 @@ def make_weights(preset, dev, world, rank):
     return cfg, W, CW
 
 
+def _graph_us(run, dev, reps=10):
+    """Capture run() into a HIP graph on a side stream, replay it `reps` times between HIP events recorded on that
+    stream; returns microseconds per replay (the per-launch dispatch gaps of the graph included)."""
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        run()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            run()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            g.replay()
+        e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def frame_bytes(cfg, B, L_talker):
+    """Algorithmic HBM bytes of one AR frame for B rows at talker cache length L_talker: every
+    talker weight once (28 layers + codec_head), per code-predictor forward (the 2-token prefill + 14 decode steps =
+    15) the 5 layers + that step's lm_head, small_to_mtp once, the talker K/V of every row (28 x 2 x Hkv x D x 2 x L)
+    and the code predictor's K/V (keys 2..16 over the 15 forwards)."""
+    t, c = cfg["talker_config"], cfg["talker_config"]["code_predictor_config"]
+
+    def layer_params(d):
+        H, I, hq, hkv, D = d["hidden_size"], d["intermediate_size"], d["num_attention_heads"], d["num_key_value_heads"], \
+            d["head_dim"]
+        return H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I
+    w_t = t["num_hidden_layers"] * layer_params(t) + t["vocab_size"] * t["hidden_size"]
+    w_cp = c["num_hidden_layers"] * layer_params(c) + c["vocab_size"] * c["hidden_size"]
+    s2m = t["hidden_size"] * c["hidden_size"] if t["hidden_size"] != c["hidden_size"] else 0
+    kv_t = t["num_hidden_layers"] * 2 * t["num_key_value_heads"] * t["head_dim"] * 2 * L_talker
+    kv_cp = sum(c["num_hidden_layers"] * 2 * c["num_key_value_heads"] * c["head_dim"] * 2 * j for j in range(2, 17))
+    return 2 * (w_t + 15 * w_cp + s2m) + B * (kv_t + kv_cp)
+
+
 def _gemv_entry(name, kernel, n_frame, Ws, M, K, N, a_dtype, o_dtype, dev, rms=False, epi=None, reps=10,
                 extra_bytes=0):
     """One decode GEMV shape timed live: a HIP graph of one launch per weight in Ws (the model's distinct per-layer

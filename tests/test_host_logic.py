@@ -51,3 +51,20 @@ def test_shard_longest_first_balances_frames():
     assert sorted(i for s in shards for i in s) == list(range(len(lengths)))
     loads = [sum(lengths[i] for i in s) for s in shards]
     assert max(loads) - min(loads) <= max(lengths)
+
+
+def test_bench_module_helpers():
+    """bench.py imports on CPU and its pure helpers compute: algorithmic bytes of a 1.7B frame."""
+    import importlib
+    import json
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    bench = importlib.import_module("bench")
+    for name in ("decode_kernel_table", "attn_oproj_entry", "_gemv_entry", "_graph_us", "_pmc_traffic",
+                 "whole_frame_roofline", "prefill_mfma", "attention_roofline", "cpu_baseline", "main", "main_vd64"):
+        assert callable(getattr(bench, name)), name
+    cfg = json.load(open(os.path.join(repo, "qwen3-tts_amd", "qwen_tts", "configs", "1.7b-customvoice", "config.json")))
+    b = bench.frame_bytes(cfg, 8, 200)
+    assert 5.0e9 < b < 6.0e9  # ~2.8 GB of talker weights + 15 code-predictor passes + K/V
