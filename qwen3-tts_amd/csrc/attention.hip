@@ -1328,11 +1328,10 @@ extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   if (a->w_dtype != a->kv_dtype || (a->w_dtype != QT_BF16 && a->w_dtype != QT_F32)) return QT_ERR_DTYPE;
   hipStream_t s = (hipStream_t)stream;
   const bool bf = a->w_dtype == QT_BF16;
-  // head-split form (a workspace was given and the shape is the code predictor's): QT_AO_HS=0 keeps the (column
-  // group, row) form (A/B); QT_AO_SPIN bounds each hand-off poll (iterations of ~1 us)
-  static const int hs_env = [] { const char* e = getenv("QT_AO_HS"); return e ? atoi(e) : 1; }();
+  // head-split form: a workspace was given and the shape is the code predictor's (the caller decides by passing ws);
+  // QT_AO_SPIN bounds each hand-off poll (iterations of ~1 us)
   static const int spin = [] { const char* e = getenv("QT_AO_SPIN"); return e ? atoi(e) : 200000; }();
-  if (hs_env && a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
+  if (a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
       a->R <= 8 && a->N % 256 == 0 && a->const_pos < a->Lmax && a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv)) {
     hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(a->N / 32 * a->Hkv), dim3(512), 0, s, AOHS{*a, spin});
     return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;

@@ -128,6 +128,8 @@ ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 # (profiles/r03_attn_oproj_rows_ab.txt); at 8 rows the fused launch wins (round 2: 155.9 -> 164.0).  QT_ATTN_OPROJ_MAX
 # overrides (A/B)
 ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
+# ... in its head-split form (qt_attn_oproj_args.ws: per-head blocks exchanging row partials) when QT_AO_HS=1
+AO_HS = os.environ.get("QT_AO_HS", "0") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -146,7 +148,7 @@ MIN_NEW_TOKENS = 2
 # ~40 GB/s, so long caches need more blocks; the frame graph is captured once per split factor and the host picks the
 # graph from its bound on the longest row's key count (tools/talker_attn_bench.py, profiles/r04_attn_long.txt).
 # QT_ATTN_SPLIT=0 keeps one block per (row, kv head) at every length (A/B)
-ATTN_SPLIT = [(448, 1), (1024, 2), (2048, 4), (1 << 30, 8)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
+ATTN_SPLIT = [(768, 1), (1536, 2), (3072, 4), (1 << 30, 8)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
 
 
 def attn_nsplit(keys: int) -> int:
@@ -180,7 +182,7 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     a = lambda *s: torch.empty(*s, dtype=st.wdt, device=dev)  # noqa: E731
     sc = {"qkv": f(R, st.qkv_w), "q": f(R, st.Hq * st.D), "att": a(R, st.Hq * st.D), "h": a(R, st.I)}
     sc["attn_oproj"] = attn_oproj and ATTN_OPROJ and _attn_oproj_ok(st)
-    if sc["attn_oproj"]:  # hand-off granules + sequence counters of the head-split fused kernel (zeroed once)
+    if sc["attn_oproj"] and AO_HS:  # hand-off granules + sequence counters of the head-split form (zeroed once)
         sc["ao_ws"] = torch.zeros(K.attn_oproj_ws_bytes(st.H, st.Hkv), dtype=torch.uint8, device=dev)
     return sc
 
