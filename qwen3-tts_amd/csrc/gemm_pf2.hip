@@ -54,6 +54,17 @@ QT_DEV unsigned lds_u32(const void* p) {
   return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
 }
 template <int N> QT_DEV void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// wait until at most min(after, MAXA) stages of G DMA instructions each remain in flight (vmcnt <= 63)
+template <int G, int MAXA>
+QT_DEV void vm_wait_stages(int after) {
+  if constexpr (MAXA <= 0) {
+    vm_wait_n<0>();
+  } else {
+    static_assert(MAXA * G <= 63, "vmcnt range");
+    if (after >= MAXA) vm_wait_n<MAXA * G>();
+    else vm_wait_stages<G, MAXA - 1>(after);
+  }
+}
 QT_DEV void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 template <int I, int N, typename F>
 QT_DEV void static_for(F&& f) {
@@ -144,8 +155,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   for (int s = 0; s < S; ++s) {
     // retire stage s (this wave's DMAs): the stages issued after it may stay in flight
     const int after = min(S - 1, s + NS - 2) - s;
-    if constexpr (NS >= 4) { if (after >= 2) vm_wait_n<2 * G>(); else if (after == 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
-    else { if (after >= 1) vm_wait_n<G>(); else vm_wait_n<0>(); }
+    vm_wait_stages<G, NS - 2>(after);
     raw_barrier();  // every wave's stage-s DMAs landed; every wave is done reading stage s - 1's buffer
     if (!(ABL & 2) && s + NS - 1 < S) issue(s + NS - 1);
     if constexpr ((ABL & 4) != 0) continue;
@@ -467,13 +477,24 @@ inline int pf2_pick(int M, int N, int K) {
   return best;
 }
 
+// LDS stages of the two small-tile configurations (QT_PF2_DEEP=1: 7 for 64 x 96 = 140 KiB, 6 for 128 x 64 = 144 KiB,
+// one block per CU): at <= 256 rows a block's loop is bound by the DMA round trip over the NS - 1 stages in flight
+// (~875 cycles per 64-deep stage of 20 KiB at NS = 4, i.e. ~55 GB/s per CU), not by its MFMAs (measurement)
+inline int pf2_deep() {
+  static const int v = [] { const char* e = getenv("QT_PF2_DEEP"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
 template <typename OT>
 void launch_pf2_auto(const GemmP& p, hipStream_t s) {
   int cfg = pf2_cfg_env();
   if (cfg == 0) cfg = pf2_pick(p.M, p.N, p.Klog);
+  const bool deep = pf2_deep() != 0;
   if (cfg == 4) launch_pf2<OT, 256, 8, 3, 4, 2>(p, s);
   else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);
+  else if (cfg == 11 && deep) launch_pf2<OT, 64, 6, 7, 2, 2>(p, s);
   else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);
+  else if (deep) launch_pf2<OT, 128, 4, 6>(p, s);
   else launch_pf2<OT, 128, 4, 3>(p, s);
 }
 #endif  // QT_PF2_PROBE
