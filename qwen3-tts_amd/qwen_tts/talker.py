@@ -144,11 +144,12 @@ PF = _hip.env_int("QT_PF", 1) != 0  # parsed as the library parses it (C atoi)
 PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
 # the generation config's min_new_tokens (M:2044-2066): EOS is suppressed while a row has generated fewer tokens
 MIN_NEW_TOKENS = 2
-# talker decode attention split-KV by cache length: (keys below which, nsplit) -- one (row, kv head) block streams
-# ~40 GB/s, so long caches need more blocks; the frame graph is captured once per split factor and the host picks the
-# graph from its bound on the longest row's key count (tools/talker_attn_bench.py, profiles/r04_attn_long.txt).
-# QT_ATTN_SPLIT=0 keeps one block per (row, kv head) at every length (A/B)
-ATTN_SPLIT = [(768, 1), (1536, 2), (3072, 4), (1 << 30, 8)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
+# talker decode attention split-KV by cache length: (keys below which, nsplit).  B = 8, 1.7B (tools/talker_attn_bench.py,
+# profiles/r04_attn_long.txt, us per launch for nsplit 1 / 2 / 4 / 8): 512 keys 11.1 / 11.4 / 12.5 / 19.2, 1024 16.5 /
+# 14.4 / 15.1 / 21.0, 2048 26.9 / 20.3 / 20.3 / 25.8, 4000 47.2 / 31.9 / 30.4 / 36.0.  The frame graph is captured once
+# per split factor and the host picks the graph from its bound on the longest row's key count.  QT_ATTN_SPLIT=0 keeps
+# one block per (row, kv head) at every length (A/B)
+ATTN_SPLIT = [(768, 1), (2048, 2), (1 << 30, 4)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
 
 
 def attn_nsplit(keys: int) -> int:
