@@ -130,18 +130,22 @@ def attn_oproj_entry(tts, B, pos=9, reps=20):
     qkv = torch.randn(B, c.qkv_w, device=dev)
     x = torch.randn(B, c.H, device=dev)
     x16 = x.to(torch.bfloat16) if eng.wdt == torch.bfloat16 else None
+    # the form the engine runs: head-split when its code-predictor scratch carries the hand-off workspace
+    ss = [s for s in eng.all_sessions() if s.cp.sc.get("ao_ws") is not None]
+    ws = torch.zeros_like(ss[0].cp.sc["ao_ws"]) if ss else None
 
     def run():
         for i, L in enumerate(c.layers):
             Kn.decode_attn_oproj(qkv, B, c.Hq, c.Hkv, c.D, L.q_norm, L.k_norm, c.eps, c.cos, c.sin, kc[i], vc[i], 18,
-                                 L.o, x, const_pos=pos, x16=x16)
+                                 L.o, x, const_pos=pos, x16=x16, ws=ws)
     us = _graph_us(run, dev, reps) / len(c.layers)
     L0 = c.layers[0]
     byt = (L0.o.w.numel() * L0.o.w.element_size() + B * c.Hkv * (pos + 1) * c.D * 2 * kc[0].element_size()
            + B * c.qkv_w * 4 + B * c.H * (4 + 4 + (2 if x16 is not None else 0)))
-    return dict(name="cp_attn_oproj", kernel=f"attn_oproj_k (code-predictor attention + o_proj + residual, {pos + 1} "
-                                              "keys)", bound="hbm", launches_per_frame=5 * (eng.G - 2), avg_us=us,
-                bytes=byt)
+    kname = "attn_oproj_hs_k (head-split" if ws is not None else "attn_oproj_k ("
+    return dict(name="cp_attn_oproj", kernel=f"{kname} code-predictor attention + o_proj + residual, {pos + 1} keys)",
+                bound="hbm", launches_per_frame=5 * (eng.G - 2), avg_us=us, bytes=byt,
+                pmc_tag="attn_oproj_hs" if ws is not None else "attn_oproj")
 
 
 def decode_kernel_table(tts, B, L_mean):
@@ -448,7 +452,8 @@ def main():
         frame_us = fr["avg_us"] if fr is not None else None
 
         def as_roof(e):
-            traffic, tsrc = _pmc_traffic(PMC_TAG[e["name"]]) if e["name"] in PMC_TAG else (None, None)
+            tag = e.get("pmc_tag", PMC_TAG.get(e["name"]))
+            traffic, tsrc = _pmc_traffic(tag) if tag else (None, None)
             return {"bound": e["bound"], "kernel": e["kernel"], "achieved": round(e["gbs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(e["frac"], 4), "traffic": traffic, "traffic_source": tsrc,
                     "avg_launch_us": round(e["avg_us"], 2), "bytes_per_launch": int(e["bytes"]),

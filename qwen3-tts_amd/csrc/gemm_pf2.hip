@@ -477,24 +477,16 @@ inline int pf2_pick(int M, int N, int K) {
   return best;
 }
 
-// LDS stages of the two small-tile configurations (QT_PF2_DEEP=1: 7 for 64 x 96 = 140 KiB, 6 for 128 x 64 = 144 KiB,
-// one block per CU): at <= 256 rows a block's loop is bound by the DMA round trip over the NS - 1 stages in flight
-// (~875 cycles per 64-deep stage of 20 KiB at NS = 4, i.e. ~55 GB/s per CU), not by its MFMAs (measurement)
-inline int pf2_deep() {
-  static const int v = [] { const char* e = getenv("QT_PF2_DEEP"); return e ? atoi(e) : 0; }();
-  return v;
-}
-
 template <typename OT>
 void launch_pf2_auto(const GemmP& p, hipStream_t s) {
   int cfg = pf2_cfg_env();
   if (cfg == 0) cfg = pf2_pick(p.M, p.N, p.Klog);
-  const bool deep = pf2_deep() != 0;
+  // (deeper pipelines of the two small-tile configurations -- 7 stages of 64 x 96, 6 of 128 x 64, one block per CU --
+  // measured slower at 24..680 rows: gate-up 160 rows 25.4 -> 37.9 us, qkv 680 rows 26.2 -> 37.1;
+  // profiles/r04_pf2_deep_ab.txt)
   if (cfg == 4) launch_pf2<OT, 256, 8, 3, 4, 2>(p, s);
   else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);
-  else if (cfg == 11 && deep) launch_pf2<OT, 64, 6, 7, 2, 2>(p, s);
   else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);
-  else if (deep) launch_pf2<OT, 128, 4, 6>(p, s);
   else launch_pf2<OT, 128, 4, 3>(p, s);
 }
 #endif  // QT_PF2_PROBE

@@ -128,8 +128,10 @@ ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
 # (profiles/r03_attn_oproj_rows_ab.txt); at 8 rows the fused launch wins (round 2: 155.9 -> 164.0).  QT_ATTN_OPROJ_MAX
 # overrides (A/B)
 ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
-# ... in its head-split form (qt_attn_oproj_args.ws: per-head blocks exchanging row partials) when QT_AO_HS=1
-AO_HS = os.environ.get("QT_AO_HS", "0") == "1"
+# ... in its head-split form (qt_attn_oproj_args.ws: per-(column group, kv head) blocks exchanging row partials): 2.5x
+# less L2 -> CU traffic than the (column group, row) form (profiles/r04_pmc_attn_oproj*.json), 7.71 -> 7.03 us per
+# launch, bench 200.2 -> 202.8 audio-s/s (profiles/r04_bench_ab_ao_hs.txt).  QT_AO_HS=0 keeps the other form (A/B)
+AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
