@@ -593,245 +593,6 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
   if (p.finished && p.eos_id >= 0 && tok == p.eos_id) p.finished[r] = 1;
 }
 
-// One wave per row (V <= 3072): greedy, and sampling with 1 <= top_k <= 64 without top-p (the generate() defaults) -- the row's
-// block-wide phases of sample_k (5+ barriers, LDS round trips between its 4 waves) were ~7 us of its ~9.5 us.  Lane l
-// holds tokens 256 j + 4 l + e (16-byte loads).  Sampling: the row maximum M of s / T; a 256-bin histogram of
-// (M - s/T) * 16 in LDS gives the boundary bin of the k-th largest score; the boundary bin's scores (<= 64, compacted
-// by ballot) give the exact k-th largest value vk; the token is the Gumbel-max over {s >= vk} with sample_k's Philox
-// keys (seed, step, substep, row, token) -- the same kept set and the same draws as sample_k's fast paths, so the same
-// token.  Rows whose top k reach beyond the histogram or tie in bulk at the boundary find vk by the MSB-first key
-// search over all keys instead (kth_step: exact, slower).
-template <int PER4>
-__global__ __launch_bounds__(64) void sample_w_k(SK pk) {
-  const qt_sample_args& p = pk.a;
-  constexpr int PER = 4 * PER4;
-  __shared__ int hist[256];
-  __shared__ float bnd[64];
-  const int r = blockIdx.x, lane = threadIdx.x;
-  const int V = p.V;
-  const float* lg = p.logits + (long long)r * p.ld;
-  const bool pen = p.seen && p.rep_penalty != 1.0f;
-  const unsigned char* sr = pen ? p.seen + (long long)r * V : (const unsigned char*)lg;
-  const int* ngp = p.n_generated ? p.n_generated + r * p.ctr_stride : (const int*)lg;
-  const int* stpp = p.step ? p.step + r * p.ctr_stride : (const int*)lg;
-  const int* prp = p.philox_row ? p.philox_row + r : (const int*)lg;
-  const unsigned char* fnp = p.finished ? p.finished + r : (const unsigned char*)lg;
-  const unsigned long long* sdp = p.seed_ptr ? p.seed_ptr : (const unsigned long long*)lg;
-  // every prologue load issued before the first use (clamped addresses: no branch around a load); the logits row is
-  // 16-byte aligned when ld % 4 == 0 (host-checked)
-  f32x4_t sv[PER4];
-  unsigned snv[PER4];
-#pragma unroll
-  for (int j = 0; j < PER4; ++j) sv[j] = *(const f32x4_t*)(lg + min(256 * j + 4 * lane, V - 4));
-#pragma unroll
-  for (int j = 0; j < PER4; ++j) snv[j] = *(const unsigned*)(sr + (pen ? min(256 * j + 4 * lane, V - 4) : 0));
-  const int ngr = __hip_atomic_load(ngp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int str = __hip_atomic_load(stpp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int fnr = *fnp;
-  const unsigned long long sdv = __hip_atomic_load(sdp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int prr = __hip_atomic_load(prp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int ngen = p.n_generated ? ngr : 1 << 30;
-  const unsigned stp = p.step ? (unsigned)str : 0u;
-  const int finv = p.finished ? fnr : 0;
-  const unsigned long long seed = p.seed_ptr ? sdv : p.seed;
-  const unsigned prow = p.philox_row ? (unsigned)prr : (unsigned)(p.row_base + r);
-  const bool eos_mask = p.eos_id >= 0 && (ngen < p.min_new_tokens || p.ignore_eos);
-  float s[PER];
-#pragma unroll
-  for (int j = 0; j < PER4; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int v = 256 * j + 4 * lane + e;
-      float x = sv[j][e];
-      if (pen && ((snv[j] >> (8 * e)) & 0xFFu)) x = x < 0.f ? x * p.rep_penalty : x / p.rep_penalty;
-      if ((eos_mask && v == p.eos_id) || (v >= p.suppress_lo && v < p.suppress_hi && v != p.suppress_keep) || v >= V)
-        x = -INFINITY;
-      s[4 * j + e] = x;
-    }
-  auto tok_of = [&](int i) { return 256 * (i >> 2) + 4 * lane + (i & 3); };
-  auto wave_argmax = [&](float& best, int& bi) {  // (max, lowest index) over the wave, wave-uniform result
-    argmax_dpp<0xB1>(best, bi);
-    argmax_dpp<0x4E>(best, bi);
-    argmax_dpp<0x141>(best, bi);
-    argmax_dpp<0x140>(best, bi);  // every lane of a 16-lane row holds its row's result
-    float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 0));
-    int i0 = __builtin_amdgcn_readlane(bi, 0);
-#pragma unroll
-    for (int rr = 16; rr < 64; rr += 16) {
-      const float ob = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), rr));
-      const int oi = __builtin_amdgcn_readlane(bi, rr);
-      if (ob > b || (ob == b && oi < i0)) { b = ob; i0 = oi; }
-    }
-    best = b;
-    bi = i0;
-  };
-  int tok;
-  if (!p.do_sample) {
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = tok_of(i);
-      if (v < V && (s[i] > best || (s[i] == best && v < bi))) { best = s[i]; bi = v; }
-    }
-    wave_argmax(best, bi);
-    tok = bi == 0x7fffffff ? 0 : bi;
-  } else {
-    const float invT = (p.temperature > 0.f && p.temperature != 1.0f) ? 1.0f / p.temperature : 1.0f;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) { s[i] *= invT; mx = fmaxf(mx, s[i]); }
-    const float M = wave_max(mx);
-    const int k = p.top_k;
-    constexpr float HB = 16.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hist[lane * 4 + i] = 0;
-    __syncthreads();  // (one wave: orders the LDS accesses)
-    int bin[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const float d = (M - s[i]) * HB;  // >= 0; -inf scores give +inf
-      bin[i] = (tok_of(i) < V && d < 256.f) ? (int)d : 256;
-      if (bin[i] < 256) atomicAdd(&hist[bin[i]], 1);
-    }
-    __syncthreads();
-    int h[4], loc = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { h[i] = hist[lane * 4 + i]; loc += h[i]; }
-    int scan = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(scan, o, 64);
-      if (lane >= o) scan += y;
-    }
-    const int excl = scan - loc;
-    int bs = -1, above = 0;
-    {
-      int b = -1, c = excl;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (b < 0) {
-          if (c + h[i] >= k) b = lane * 4 + i;
-          else c += h[i];
-        }
-      }
-      const bool cross = excl < k && scan >= k;
-      const unsigned long long cm = __ballot(cross);
-      if (cm) {
-        const int src = __ffsll((long long)cm) - 1;
-        bs = __shfl(b, src, 64);
-        above = __shfl(c, src, 64);
-      }
-    }
-    // the boundary bin's scores, compacted into LDS by ballot (a bin of > 64 scores takes the exact key search)
-    int nb = 0;
-    if (bs >= 0) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const bool in = bin[i] == bs;
-        const unsigned long long m = __ballot(in);
-        const int pos = nb + __popcll(m & ((1ull << lane) - 1ull));
-        if (in && pos < 64) bnd[pos] = s[i];
-        nb += __popcll(m);
-      }
-    }
-    __syncthreads();
-    float vk;
-    if (bs >= 0 && nb <= 64) {
-      const int need = k - above;  // 1 <= need <= nb
-      const float mine = lane < nb ? bnd[lane] : -INFINITY;
-      int gt = 0, ge = 0;
-      for (int i = 0; i < nb; ++i) {
-        const float o = bnd[i];
-        gt += o > mine ? 1 : 0;
-        ge += o >= mine ? 1 : 0;
-      }
-      const unsigned long long kb = __ballot(lane < nb && gt < need && need <= ge);
-      vk = __shfl(mine, kb ? __ffsll((long long)kb) - 1 : 0, 64);
-    } else {  // exact k-th largest key over all keys (MSB-first, 2 bits per step, wave counts)
-      unsigned key[PER];
-      int nv = 0;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        key[i] = tok_of(i) < V ? okey(s[i]) : 0u;
-        nv += key[i] != 0u;
-      }
-      int cur = wave_sum_i(nv);
-      unsigned t = 0u;
-      for (int bit = 30; bit >= 0 && cur != k; bit -= 2) kth_step<PER>(key, k, bit, t, cur);
-      // smallest kept key: the largest key value that still has >= k keys at or above it (t is that prefix)
-      unsigned kmin = 0xFFFFFFFFu;
-#pragma unroll
-      for (int i = 0; i < PER; ++i)
-        if (key[i] != 0u && key[i] >= t) kmin = min(kmin, key[i]);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o, 64));
-      vk = okey_inv(kmin);
-    }
-    // Gumbel-max over the kept set {s >= vk} (ties kept, TopKLogitsWarper); masked (-inf) scores are never drawn
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = tok_of(i);
-      if (v < V && s[i] >= vk && s[i] > -INFINITY) {
-        const float u = philox_uniform4(seed, stp, (unsigned)p.substep, prow, (unsigned)v);
-        const float g = okey_inv(okey(s[i])) - __logf(-__logf(u));
-        if (g > best || (g == best && v < bi)) { best = g; bi = v; }
-      }
-    }
-    wave_argmax(best, bi);
-    tok = bi == 0x7fffffff ? 0 : bi;
-  }
-  if (finv) tok = p.eos_id;
-  if (p.force) {  // teacher forcing: record this path's choice, continue with the forced token
-    const long long off = (long long)r * p.codes_ld + (long long)((int)stp + p.codes_step_off) * p.codes_w + p.codes_col;
-    if (lane == 0) p.pick[off] = tok;
-    tok = p.force[off];
-  }
-  if (p.emb_table) {  // next-step input row(s), as sample_k writes them
-    const float* src = p.emb_table + (long long)tok * p.emb_dim;
-    float* dst = p.emb_out + (long long)r * p.emb_ld;
-    bf16_t* d16 = p.emb_out16 ? (bf16_t*)p.emb_out16 + (long long)r * p.emb_ld16 : nullptr;
-    const bool two = p.emb2_table != nullptr;
-    const float* src2 = two ? p.emb2_table + (long long)tok * p.emb2_dim : src;
-    const int n2 = two ? p.emb2_dim : 0;
-    float* dst2 = two ? p.emb2_out + (long long)r * p.emb2_ld : nullptr;
-    constexpr int G = 4;  // float4s per lane in flight per pass
-    for (int i0 = 0; i0 < p.emb_dim; i0 += 64 * 4 * G) {
-      f32x4_t v[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g) v[g] = *(const f32x4_t*)(src + min(i0 + (g * 64 + lane) * 4, p.emb_dim - 4));
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int i = i0 + (g * 64 + lane) * 4;
-        if (i < p.emb_dim) {
-          *(f32x4_t*)(dst + i) = v[g];
-          if (d16) *(uint2*)(d16 + i) = uint2{pack2bf(v[g][0], v[g][1]), pack2bf(v[g][2], v[g][3])};
-        }
-      }
-    }
-    for (int i0 = 0; i0 < n2; i0 += 64 * 4 * G) {
-      f32x4_t v[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g) v[g] = *(const f32x4_t*)(src2 + min(i0 + (g * 64 + lane) * 4, n2 - 4));
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int i = i0 + (g * 64 + lane) * 4;
-        if (i < n2) *(f32x4_t*)(dst2 + i) = v[g];
-      }
-    }
-  }
-  if (lane != 0) return;
-  p.tok_out[r] = tok;
-  if (p.codes) {
-    const int st = (int)stp + p.codes_step_off;
-    p.codes[(long long)r * p.codes_ld + (long long)st * p.codes_w + p.codes_col] = tok;
-  }
-  if (p.seen) p.seen[(long long)r * V + tok] = 1;
-  if (p.finished && p.eos_id >= 0 && tok == p.eos_id) p.finished[r] = 1;
-}
-
 }  // namespace
 
 extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
@@ -845,18 +606,6 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
   const SK k{*a, stop};
-  // one wave per row for greedy and for 1 <= top_k <= 64 without top-p (QT_SAMPLE_WAVE=0: the block kernel, A/B);
-  // algo != 0 / debug_u / the measurement hook keep the block kernel's paths
-  static const int wave_env = [] { const char* e = getenv("QT_SAMPLE_WAVE"); return e ? atoi(e) : 1; }();
-  const bool wave_ok = wave_env && a->algo == 0 && a->debug_u < 0.f && stop == 0 && a->V >= 256 && a->V <= 3072 &&
-                       a->V % 4 == 0 &&
-                       a->ld % 4 == 0 && ((size_t)a->logits & 15) == 0 &&
-                       (!a->do_sample || (a->top_k >= 1 && a->top_k <= 64 && a->top_k < a->V && a->top_p >= 1.0f));
-  if (wave_ok) {
-    if (a->V <= 2048) hipLaunchKernelGGL(sample_w_k<8>, dim3(a->R), dim3(64), 0, st, k);
-    else hipLaunchKernelGGL(sample_w_k<12>, dim3(a->R), dim3(64), 0, st, k);
-    return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
-  }
   if (a->V <= NT * 8) hipLaunchKernelGGL(sample_k<8>, dim3(a->R), dim3(NT), 0, st, k);
   else if (a->V <= NT * 12) hipLaunchKernelGGL(sample_k<12>, dim3(a->R), dim3(NT), 0, st, k);
   else hipLaunchKernelGGL(sample_k<16>, dim3(a->R), dim3(NT), 0, st, k);
