@@ -280,7 +280,7 @@ int attn_dispatch(const qt_attn_args& p, hipStream_t s) {
 // K and V fragments of IC keys are loaded before any use (IC x 2 KiB in flight per group) and folded
 // into an online softmax; partial (m, l, o) merge across groups by shuffles and across waves via LDS.
 // Bytes per (row, head) = 2 * L * D * sizeof(kv): the decode-attention HBM roofline of SURVEY.md §8(d).
-template <typename KV, int D, int NREP, int NW, int NB = 2>
+template <typename KV, int D, int NREP, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) {
   // NW waves: 8 for long caches (8 x 64 lanes keeps kf/vf/o/q (~150 VGPRs) out of scratch), 4 for short ones
   // (code predictor, <= 17 keys: fewer idle waves in the merges)
@@ -307,10 +307,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
   const KV* Vc = (const KV*)p.v_cache + base;
   // raw fragments stay packed (bf16: 4 VGPRs per 8 elements) until used: IC keys in flight per group
   constexpr int RW = sizeof(KV) * 8 / 4;  // 32-bit words per 8-element fragment
-  // NB register sets in a ring: chunk i is consumed from set i % NB while chunks i + 1 .. i + NB - 1 stream into the
-  // others (NB = 2: ping-pong; 4 for long caches, where one chunk in flight per wave left a block at ~35 GB/s --
-  // Little's law on the ~2 us HBM round trip, profiles/r04_attn_long.txt)
-  unsigned kb[NB][IC][RW], vb[NB][IC][RW];
+  unsigned kr[IC][RW], vr[IC][RW];   // chunk being consumed
+  unsigned kn[IC][RW], vn[IC][RW];   // next chunk, in flight while the current one is consumed
   auto load_into = [&](int j0, unsigned (*kd)[RW], unsigned (*vd)[RW]) {  // cached keys only
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
@@ -325,7 +323,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
       }
     }
   };
-  auto load_chunk = [&](int j0) { load_into(j0, kb[0], vb[0]); };
+  auto load_chunk = [&](int j0) { load_into(j0, kr, vr); };
   auto unpack = [&](const unsigned* r, float* o8) {
     if constexpr (sizeof(KV) == 2) {
 #pragma unroll
@@ -435,29 +433,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_k(qt_decode_attn_args p) 
   };
   constexpr int GIC = G * IC;
   // The prefetches are unconditional (clamped addresses): a branch around them made hipcc's merged wait counts
-  // drain the prefetch before the current chunk was consumed, serialising the round trips.
-  if constexpr (NB == 2) {  // (this exact form: the generic ring below costs the ping-pong 32 more VGPRs)
-    for (int j0 = j_lo + gid; j0 < j_hi; j0 += 2 * GIC) {
-      load_into(j0 + GIC, kb[1], vb[1]);
-      consume(kb[0], vb[0], j0);
-      if (j0 + GIC >= j_hi) break;
-      load_into(j0 + 2 * GIC, kb[0], vb[0]);
-      consume(kb[1], vb[1], j0 + GIC);
-    }
-  } else {
-#pragma unroll
-    for (int b = 1; b < NB - 1; ++b) load_into(j_lo + gid + b * GIC, kb[b], vb[b]);
-    bool more = true;
-    for (int j0 = j_lo + gid; more && j0 < j_hi; j0 += NB * GIC) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        if (more) {
-          load_into(j0 + (b + NB - 1) * GIC, kb[(b + NB - 1) % NB], vb[(b + NB - 1) % NB]);
-          consume(kb[b], vb[b], j0 + b * GIC);
-          more = j0 + (b + 1) * GIC < j_hi;
-        }
-      }
-    }
+  // drain the prefetch before the current chunk was consumed, serialising the two round trips.
+  for (int j0 = j_lo + gid; j0 < j_hi; j0 += 2 * GIC) {
+    load_into(j0 + GIC, kn, vn);
+    consume(kr, vr, j0);
+    if (j0 + GIC >= j_hi) break;
+    load_into(j0 + 2 * GIC, kr, vr);
+    consume(kn, vn, j0 + GIC);
   }
   // merge lane groups inside the wave (ds_bpermute butterflies: the permlane transpose-reduce GroupMerge was
   // measured 3 us slower in this kernel, 11.3 vs 8.2 us at 210 keys, tools/talker_attn_bench.py)
@@ -1278,24 +1260,16 @@ int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
   dim3 g(a.R, a.Hkv, ns);
   static const int nw_env = [] { const char* e = getenv("QT_ATTN_SHORT"); return e ? atoi(e) : -1; }();
   const bool short_cache = nw_env >= 0 ? nw_env != 0 : a.Lmax <= 64;  // 4 waves cover <= 64 keys in one pass
-  // register-set ring depth: 4 for the split (long-cache) launches, 2 otherwise; QT_ATTN_NB = 2 / 4 forces (A/B)
-  static const int nb_env = [] { const char* e = getenv("QT_ATTN_NB"); return e ? atoi(e) : 0; }();
-  const bool deep = nb_env ? nb_env >= 4 : ns > 1;
   switch (a.Hq / a.Hkv) {
     case 1:
       if (short_cache) hipLaunchKernelGGL((attn_decode_k<KV, D, 1, 4>), g, dim3(256), 0, s, a);
-      else if (deep) hipLaunchKernelGGL((attn_decode_k<KV, D, 1, 8, 4>), g, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((attn_decode_k<KV, D, 1, 8>), g, dim3(512), 0, s, a);
       break;
     case 2:
       if (short_cache) hipLaunchKernelGGL((attn_decode_k<KV, D, 2, 4>), g, dim3(256), 0, s, a);
-      else if (deep) hipLaunchKernelGGL((attn_decode_k<KV, D, 2, 8, 4>), g, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((attn_decode_k<KV, D, 2, 8>), g, dim3(512), 0, s, a);
       break;
-    case 4:
-      if (deep) hipLaunchKernelGGL((attn_decode_k<KV, D, 4, 8, 4>), g, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((attn_decode_k<KV, D, 4, 8>), g, dim3(512), 0, s, a);
-      break;
+    case 4: hipLaunchKernelGGL((attn_decode_k<KV, D, 4, 8>), g, dim3(512), 0, s, a); break;
     default: return QT_ERR_SHAPE;
   }
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;

@@ -491,8 +491,8 @@ def test_decode_attention_matches_two_kernel_path(D, hq, hkv, L, kvdt):
     Kn.decode_attention(qkv, B, hq, hkv, D, qn, kn, 1e-6, cos, sin, same, rb, same, zero, kc5, vc5, L + 3, a5,
                         const_pos=L - 1)
     assert torch.equal(a4, a5) and torch.equal(kc4, kc5) and torch.equal(vc4, vc5)
-    # split-KV (nsplit blocks per (row, kv head), deterministic merge; these launches stream through a 4-deep ring of
-    # register sets -- at 2100 keys more than 4 chunks per split, so the ring wraps) == single block, reproducible
+    # split-KV (nsplit blocks per (row, kv head), deterministic merge) == single block, bitwise reproducible (2100 keys:
+    # several ping-pong chunks per split)
     for ns in (2, 3, 8):
         ws = torch.zeros(Kn.decode_attn_ws_bytes(B, hq, hkv, D, ns), dtype=torch.uint8, device=dev)
         outs = []
