@@ -940,9 +940,21 @@ struct AOHS {
   qt_attn_oproj_args a;
   int spin_limit;
   int stop;  // measurement hook (QT_AO_STOP, as attn_oproj_k): end after phase 1..4 (before any hand-off); 0 = full
+  int cg_log2;  // log2(column groups) when a power of two (block -> (head, group) by shifts), else -1
 };
 
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// two floats -> bf16 pair (low = a) by v_cvt_pk_bf16_f32 (round to nearest even; one instruction for f2bf's four)
+QT_DEV unsigned pack2bf_rne(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+
+QT_DEV u32x4_t ld_u32x4(const void* p) { return *(const u32x4_t*)p; }
+QT_DEV unsigned ld_u32(const void* p) { return *(const unsigned*)p; }
 
 QT_DEV size_t aohs_gran_off(int CG, int nk) { return 256 + ((size_t)CG * nk * 4 + 255) / 256 * 256; }
 
@@ -954,16 +966,20 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   constexpr int LPK = D / 8, GPW = 64 / LPK, IC = 4;
   static_assert(FPW >= 1 && KTS % FPW == 0 && GPW >= NREP + 2, "head-split attn_oproj shape");
   constexpr int ALD = KS + 8;  // bf16 A-tile row stride (16 B pad)
-  __shared__ float qs[NW][NREP][D];
-  __shared__ float kn[NW][D], vn[NW][D];
+  // q and the new key as bf16 pairs (the cache's format: v_dot2 scores), the new value as fp32
+  __shared__ __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];
+  __shared__ __attribute__((aligned(16))) unsigned kn2[NW][D / 2];
+  __shared__ float vn[NW][D];
   __shared__ __attribute__((aligned(16))) bf16_t att[NW][ALD];
   __shared__ float red[NW][64][4];
   __shared__ float part[NW][NC];
   __shared__ float gath[8][NC];
   __shared__ int fail_sh;
   const int R = p.R, nq = p.Hq, nk = p.Hkv;
-  const int CG = gridDim.x / nk;
-  const int h = blockIdx.x / CG, cg = blockIdx.x % CG;
+  const int lg = pk.cg_log2;  // (the runtime divisions cost ~60 scalar instructions ahead of the first load)
+  const int CG = lg >= 0 ? 1 << lg : (int)gridDim.x / nk;
+  const int h = lg >= 0 ? (int)blockIdx.x >> lg : (int)blockIdx.x / CG;
+  const int cg = lg >= 0 ? (int)blockIdx.x & (CG - 1) : (int)blockIdx.x % CG;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lm = lane & 15, lk = lane >> 4;
   const int grp = lane / LPK, sub = lane % LPK;
@@ -978,16 +994,18 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   unsigned long long* gran = (unsigned long long*)((char*)p.ws + aohs_gran_off(CG, nk));
   const int ktiles = nq * D / KT;
 
-  // 1. every load, in the order the phases need them (inline asm, counted waits -- see attn_oproj_k)
+  // 1. every load, in the order the phases need them.  Plain loads: hipcc's own counted waits retire them (inline-asm
+  // loads + explicit waits let the register allocator copy a destination before its wait -- stale data,
+  // nondeterministic results; tools/asm_load_hazards.py)
   u32x4_t xq[2], nwr[2], cvr[2], svr[2];
   {
     const float* nwp = vsel < NREP ? (p.q_norm ? p.q_norm + e0 : xsrc) : (p.k_norm ? p.k_norm + e0 : xsrc);
     const float* cs = p.cos_tab + (long long)kvpos * half + ec;
     const float* sn = p.sin_tab + (long long)kvpos * half + ec;
-    asm_ld16(xq[0], xsrc); asm_ld16(xq[1], xsrc + 4);
-    asm_ld16(nwr[0], nwp); asm_ld16(nwr[1], nwp + 4);
-    asm_ld16(cvr[0], cs); asm_ld16(cvr[1], cs + 4);
-    asm_ld16(svr[0], sn); asm_ld16(svr[1], sn + 4);
+    xq[0] = ld_u32x4(xsrc); xq[1] = ld_u32x4(xsrc + 4);
+    nwr[0] = ld_u32x4(nwp); nwr[1] = ld_u32x4(nwp + 4);
+    cvr[0] = ld_u32x4(cs); cvr[1] = ld_u32x4(cs + 4);
+    svr[0] = ld_u32x4(sn); svr[1] = ld_u32x4(sn + 4);
   }
   const long long kvbase = ((long long)r * nk + h) * p.Lmax * D;
   u32x4_t kq[IC], vq[IC];
@@ -996,36 +1014,31 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
     return (const bf16_t*)(isv ? p.v_cache : p.k_cache) + kvbase + (long long)jj * D + sub * 8;
   };
 #pragma unroll
-  for (int c = 0; c < IC; ++c) { asm_ld16(kq[c], kv_addr(0, c, false)); asm_ld16(vq[c], kv_addr(0, c, true)); }
+  for (int c = 0; c < IC; ++c) { kq[c] = ld_u32x4(kv_addr(0, c, false)); vq[c] = ld_u32x4(kv_addr(0, c, true)); }
   const int f0 = w * FPW, tw = f0 / KTS, kt0 = f0 % KTS;
   u32x4_t wv[FPW];
   {
     const bf16_t* wp = (const bf16_t*)p.w_o + ((size_t)(cg * NT + tw) * ktiles + (size_t)h * KTS + kt0) * 64 * E +
                        lane * E;
 #pragma unroll
-    for (int i = 0; i < FPW; ++i) asm_ld16(wv[i], wp + (size_t)i * 64 * E);
+    for (int i = 0; i < FPW; ++i) wv[i] = ld_u32x4(wp + (size_t)i * 64 * E);
   }
   // the granule this lane publishes (row w, column lane & 31): its previous tag
   const size_t my_g = ((size_t)(cg * nk + h) * 8 + w) * NC + (lane & (NC - 1));
   u32x2_t gprev;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(gprev) : "v"(gran + my_g) : "memory");
+  gprev = *(const u32x2_t*)(gran + my_g);
   // residual of the row this block finalises (row h) at this lane's column; this block's consumed count
   unsigned xres_u, cprev;
-  asm_ld4(xres_u, p.x + (long long)min(h, R - 1) * p.ldx + cg * NC + (lane & (NC - 1)));
-  asm_ld4(cprev, cnt + cg * nk + h);
-  constexpr int N_X = 2, N_T = 1, N_W = FPW, N_KV = 2 * IC;
+  xres_u = ld_u32(p.x + (long long)min(h, R - 1) * p.ldx + cg * NC + (lane & (NC - 1)));
+  cprev = ld_u32(cnt + cg * nk + h);
+  __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any of the phases' math
   if (pk.stop == 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    reg_fence(xq[0]); reg_fence(kq[0]); reg_fence(wv[0]); reg_fence(gprev); reg_fence(xres_u); reg_fence(cprev);
     if ((xq[0][0] ^ kq[0][0] ^ wv[0][0] ^ gprev[0] ^ xres_u ^ cprev) == 0x9E3779B9u) p.x[0] = 0.f;
     return;
   }
 
   // 2. q/k RMSNorm + RoPE of head h's vectors of row r (v passes through), into LDS
   {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_KV + N_W + N_T + N_X) : "memory");
-    reg_fence(xq[0]); reg_fence(xq[1]); reg_fence(nwr[0]); reg_fence(nwr[1]);
-    reg_fence(cvr[0]); reg_fence(cvr[1]); reg_fence(svr[0]); reg_fence(svr[1]);
     const bool lo = e0 < half;
     float nwv[8], cv[8], sv[8], xv[8];
 #pragma unroll
@@ -1035,121 +1048,117 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
       sv[i] = __uint_as_float(svr[0][i]); sv[i + 4] = __uint_as_float(svr[1][i]);
       xv[i] = __uint_as_float(xq[0][i]); xv[i + 4] = __uint_as_float(xq[1][i]);
     }
-    if (vsel <= NREP) {
-      const bool isq = vsel < NREP;
+    {  // branch-free over the lane groups (the v group's result is discarded): a lane-divergent branch here made
+       // hipcc sink the norm-weight / cos / sin loads into it, behind a wait for the first loads (two round trips)
+      const bool isq = vsel < NREP, normed = vsel <= NREP;
+      const bool has_w = isq ? p.q_norm != nullptr : p.k_norm != nullptr;
       float ss = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) ss += xv[i] * xv[i];
       ss = group_sum_dpp<LPK>(ss);
       const float rs = rsqrtf(ss / (float)D + p.eps);
-      if (isq ? p.q_norm != nullptr : p.k_norm != nullptr) {
+      float y[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xv[i] = nwv[i] * (xv[i] * rs);
-      }
+      for (int i = 0; i < 8; ++i) y[i] = has_w ? nwv[i] * (xv[i] * rs) : xv[i];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {  // q*cos + rotate_half(q)*sin
-        const float pt = half_partner<LPK>(xv[i]);
-        xv[i] = lo ? xv[i] * cv[i] - pt * sv[i] : xv[i] * cv[i] + pt * sv[i];
+        const float pt = half_partner<LPK>(y[i]);
+        const float ro = lo ? y[i] * cv[i] - pt * sv[i] : y[i] * cv[i] + pt * sv[i];
+        xv[i] = normed ? ro : xv[i];
       }
     }
-    if (grp < NREP) {
+    if (grp <= NREP) {  // q heads, the new key: bf16 pairs (dims 2i, 2i + 1 = low, high half)
+      u32x4_t pk2;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qs[w][grp][e0 + i] = xv[i];
-    } else if (grp < NREP + 2) {  // as the cache holds them (bf16 rounding)
-      float* dst = grp == NREP ? kn[w] : vn[w];
+      for (int i = 0; i < 4; ++i) pk2[i] = pack2bf_rne(xv[2 * i], xv[2 * i + 1]);
+      *(u32x4_t*)(grp < NREP ? &qs2[w][grp][e0 / 2] : &kn2[w][e0 / 2]) = pk2;
+    } else if (grp == NREP + 1) {  // the new value as the cache holds it (bf16 rounding)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dst[e0 + i] = bf2f(f2bf(xv[i]));
+      for (int i = 0; i < 8; ++i) vn[w][e0 + i] = bf2f(f2bf(xv[i]));
     }
   }
   __syncthreads();
   if (pk.stop == 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    reg_fence(kq[0]); reg_fence(wv[0]);
-    if (qs[w][0][lane] == 1234.5f && kq[0][0] == 7u && wv[0][0] == 7u) p.x[0] = 0.f;
+    if (qs2[w][0][lane] == 12345u && kq[0][0] == 7u && wv[0][0] == 7u) p.x[0] = 0.f;
     return;
   }
   // 3. attention of (row r, head h): lane group grp owns cached keys grp, grp + GPW, ...; the new key is folded into
   // lane group 0's state; groups merge through a common max + plain sums
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_W + N_T + N_X) : "memory");
-#pragma unroll
-  for (int c = 0; c < IC; ++c) { reg_fence(kq[c]); reg_fence(vq[c]); }
   {
+    // One batch of <= GPW * IC cached keys + the new key, no running state: scores by v_dot2 on bf16 pairs (q rounded
+    // to bf16 as the reference's bf16 attention holds it), fp32 softmax per lane group, the weights rounded to bf16
+    // pairs of keys (c, c + 1) and P.V as v_dot2 over key pairs of V (v_perm regroups the cache's dim pairs);
+    // l sums the rounded weights.  The attention phase was VALU-bound (2 waves / SIMD, ~535 VALU per wave).
     const float scale = rsqrtf((float)D) * 1.4426950408889634f;  // scores in log2 units (exp2 softmax)
-    float q[NREP][8], m[NREP], l[NREP], o[NREP][8];
+    u32x4_t q2[NREP];
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) q2[j] = *(const u32x4_t*)&qs2[w][j][sub * 4];
+    const u32x4_t k2n = *(const u32x4_t*)&kn2[w][sub * 4];
+    auto dot8 = [](const u32x4_t& a, const u32x4_t& b) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // (elements copied out first: a __builtin_bit_cast of a vector-element lvalue read element 0 every time)
+        const unsigned ai = a[i], bi = b[i];
+        d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, ai), __builtin_bit_cast(bf16x2_t, bi), d, false);
+      }
+      return d;
+    };
+    float dd[NREP][IC], dn[NREP];
 #pragma unroll
     for (int j = 0; j < NREP; ++j) {
-      m[j] = -INFINITY; l[j] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { q[j][i] = qs[w][j][sub * 8 + i] * scale; o[j][i] = 0.f; }
-    }
-    {  // one batch: the host routes <= GPW * IC cached keys here (no loop, so no compiler wait at a loop preheader)
-      float vf[IC][8], dd[NREP][IC];
+      dn[j] = group_sum_dpp<LPK>(dot8(q2[j], k2n)) * scale;  // the new key (every lane group computes it)
 #pragma unroll
       for (int c = 0; c < IC; ++c) {
-        const int jj = c * GPW + grp;
-        float kf[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          kf[2 * i] = __uint_as_float(kq[c][i] << 16); kf[2 * i + 1] = __uint_as_float(kq[c][i] & 0xFFFF0000u);
-          vf[c][2 * i] = __uint_as_float(vq[c][i] << 16); vf[c][2 * i + 1] = __uint_as_float(vq[c][i] & 0xFFFF0000u);
-        }
-        if (jj >= nc) {  // masked key: weight exactly 0, keep 0 * v finite
-#pragma unroll
-          for (int i = 0; i < 8; ++i) vf[c][i] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < NREP; ++j) {
-          float d = 0.f;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
-          d = group_sum_dpp<LPK>(d);
-          dd[j][c] = jj < nc ? d : -INFINITY;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        float mn = m[j];
-#pragma unroll
-        for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
-        if (mn == -INFINITY) continue;
-        const float f = exp2_hw(m[j] - mn);
-        float e[IC], es = 0.f;
-#pragma unroll
-        for (int c = 0; c < IC; ++c) { e[c] = exp2_hw(dd[j][c] - mn); es += e[c]; }
-        l[j] = l[j] * f + es;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float acc = o[j][i] * f;
-#pragma unroll
-          for (int c = 0; c < IC; ++c) acc += e[c] * vf[c][i];
-          o[j][i] = acc;
-        }
-        m[j] = mn;
+        const float d = group_sum_dpp<LPK>(dot8(q2[j], kq[c])) * scale;
+        dd[j][c] = c * GPW + grp < nc ? d : -INFINITY;  // masked keys read a clamped, finite cached key: weight 0
       }
     }
-    {  // the new key (LDS), lane group 0
-      float kf[8], vv[8];
+    // V regrouped to key pairs: vp[pr][i] = (v[2pr][2i], v[2pr + 1][2i]), vp[pr][4 + i] = (v[2pr][2i+1], v[2pr+1][2i+1])
+    unsigned vp[IC / 2][8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { kf[i] = kn[w][sub * 8 + i]; vv[i] = vn[w][sub * 8 + i]; }
+    for (int pr = 0; pr < IC / 2; ++pr)
 #pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        float d = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d += q[j][i] * kf[i];
-        d = group_sum_dpp<LPK>(d);
-        if (grp == 0) {
-          const float mn = fmaxf(m[j], d);
-          const float f = exp2_hw(m[j] - mn), e = exp2_hw(d - mn);
-          l[j] = l[j] * f + e;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[j][i] = o[j][i] * f + e * vv[i];
-          m[j] = mn;
-        }
+      for (int i = 0; i < 4; ++i) {
+        vp[pr][i] = __builtin_amdgcn_perm(vq[2 * pr + 1][i], vq[2 * pr][i], 0x05040100u);
+        vp[pr][4 + i] = __builtin_amdgcn_perm(vq[2 * pr + 1][i], vq[2 * pr][i], 0x07060302u);
       }
+    float vnf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vnf[i] = vn[w][sub * 8 + i];
+    float m[NREP], l[NREP], o[NREP][8];
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      float mn = dn[j];
+#pragma unroll
+      for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
+      const float en = grp == 0 ? exp2_hw(dn[j] - mn) : 0.f;  // the new key counts once (lane group 0)
+      unsigned ep[IC / 2];
+#pragma unroll
+      for (int pr = 0; pr < IC / 2; ++pr) {
+        const float ea = exp2_hw(dd[j][2 * pr] - mn), eb = exp2_hw(dd[j][2 * pr + 1] - mn);
+        ep[pr] = pack2bf_rne(ea, eb);
+      }
+      float ls = en;
+#pragma unroll
+      for (int pr = 0; pr < IC / 2; ++pr)
+        ls = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, ep[pr]),
+                                             __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls, false);
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        float acc = en * vnf[d];
+        const int vi = (d & 1) * 4 + (d >> 1);
+#pragma unroll
+        for (int pr = 0; pr < IC / 2; ++pr)
+          acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, ep[pr]),
+                                                __builtin_bit_cast(bf16x2_t, vp[pr][vi]), acc, false);
+        o[j][d] = acc;
+      }
+      m[j] = mn; l[j] = ls;
     }
     GroupMerge<LPK, NREP> gm;
     gm.run(m, l, o);
-    gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = f2bf(ov / lv); });
+    gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = f2bf(ov * __builtin_amdgcn_rcpf(lv)); });
   }
   __syncthreads();
   if (pk.stop == 3) {
@@ -1159,9 +1168,6 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   }
   // 4. head h's K-slice of o_proj for the block's 32 columns: wave w multiplies fragments f0 .. f0 + FPW - 1 (column
   // tile tw); MFMA rows = batch rows (rows >= NW zero)
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_T + N_X) : "memory");
-#pragma unroll
-  for (int i = 0; i < FPW; ++i) reg_fence(wv[i]);
   {
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1177,8 +1183,6 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   __syncthreads();
   // 5. row w's partial (thread (w, c < NC)): the column tile's waves summed in wave order; publish it to the block of
   // head w (rows < R other than h), keep row h
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_X) : "memory");
-  reg_fence(gprev);
   if (lane < NC) {
     const int c = lane, t = c >> 4, cc = c & 15;
     float v = 0.f;
@@ -1193,8 +1197,6 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   }
   if (pk.stop == 4) return;
   // 6. block of head h < R: the other heads' partials of row h, then the row
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  reg_fence(xres_u); reg_fence(cprev);
   if (h < R) {
     const unsigned want = cprev + 1u;
     if (tid < (nk - 1) * NC) {
@@ -1226,8 +1228,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   // 7. the new k / v of (row w, head h) into the caches (one column group appends)
   if (cg == 0 && w < R && lane < D) {
     const long long o = (((long long)w * nk + h) * p.Lmax + kvpos) * D + lane;
-    ((bf16_t*)p.k_cache)[o] = f2bf(kn[w][lane]);
-    if (lane + 64 < D) ((bf16_t*)p.k_cache)[o + 64] = f2bf(kn[w][lane + 64]);
+    if (lane < D / 2) ((unsigned*)p.k_cache)[(o - lane) / 2 + lane] = kn2[w][lane];  // the bf16 pairs (row start even)
     ((bf16_t*)p.v_cache)[o] = f2bf(vn[w][lane]);
     if (lane + 64 < D) ((bf16_t*)p.v_cache)[o + 64] = f2bf(vn[w][lane + 64]);
   }
@@ -1355,7 +1356,10 @@ extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   if (a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
       a->R <= 8 && a->N % 256 == 0 && a->const_pos < a->Lmax && a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv)) {
     static const int stop = [] { const char* e = getenv("QT_AO_STOP"); return e ? atoi(e) : 0; }();
-    hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(a->N / 32 * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop});
+    const int cgs = a->N / 32;
+    static const int nolg = [] { const char* e = getenv("QT_AO_NOLG"); return e ? atoi(e) : 0; }();
+    const int lg = !nolg && (cgs & (cgs - 1)) == 0 ? __builtin_ctz((unsigned)cgs) : -1;
+    hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(cgs * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop, lg});
     return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
   }
   switch (a->D) {
