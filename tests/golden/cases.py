@@ -57,6 +57,10 @@ def full_cases():
         # configs[2]: 1.7B CustomVoice, B=8 x 200-token prompts, streaming text (trailing text fed per frame)
         "cv17_b8_stream": dict(preset="1.7b-customvoice", idx=60, texts=[200] * 8, languages=["english"] * 8,
                                speakers=FULL_SPEAKERS, non_streaming_mode=False, max_new_tokens=33),
+        # configs[2] at the bench's length: 1.7B CustomVoice, 2 rows x 200 / 150-token prompts, streaming text, 256
+        # frames (talker caches up to ~460 keys: the decode attention's length range in bench.py)
+        "cv17_b2_long": dict(preset="1.7b-customvoice", idx=64, texts=[200, 150], languages=["english", "chinese"],
+                             speakers=FULL_SPEAKERS[:2], non_streaming_mode=False, max_new_tokens=257),
         # configs[1]: 0.6B CustomVoice, 1 utterance of 120 text tokens, non-streaming (Identity small_to_mtp, M:1174)
         "cv06_b1_nonstream": dict(preset="0.6b-customvoice", idx=61, texts=[120], languages=["english"],
                                   speakers=["vivian"], non_streaming_mode=True, max_new_tokens=49),

@@ -9,6 +9,8 @@ the reference's own greedy codes (tests/golden/full_<case>.npz, written by make_
                      (configs[3] shape: left-padded batch, instruct prepended, M:2076-2080)
   base17_b2_clone    1.7B-Base voice clone, one ICL row (40-token reference text, 38 reference frames) and one
                      x-vector-only row, streaming text, 24 frames (configs[4] shape: M:1968-2019, 2102-2106)
+  cv17_b2_long       1.7B CustomVoice, 2 rows x 200 / 150-token prompts, streaming text, 256 frames (the bench's
+                     length: talker caches up to ~460 keys, every code-predictor step of 256 frames)
 
 Every greedy pick of the reference (talker cb0 and the code predictor's 15, [B, frames, 16]) carries its top-2
 margin of the processed scores (from the oracle, itself asserted bit-identical to the reference's codes when the
@@ -128,7 +130,7 @@ def _check_free_run(codes, ref, margins, tol, label, require_full=False):
     return div
 
 
-KEYS = ["cv06_b1_nonstream", "cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone"]
+KEYS = ["cv06_b1_nonstream", "cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone", "cv17_b2_long"]
 
 
 @pytest.mark.parametrize("key", KEYS)
