@@ -957,18 +957,8 @@ QT_DEV u32x4_t ld_u32x4(const void* p) { return *(const u32x4_t*)p; }
 QT_DEV unsigned ld_u32(const void* p) { return *(const unsigned*)p; }
 
 QT_DEV size_t aohs_gran_off(int CG, int nk) { return 256 + ((size_t)CG * nk * 4 + 255) / 256 * 256; }
-// fused q/k/v exchange (after the o_proj granules): per-(block, row) gather counts, then the q/k/v granules
-// [kv head][column tile][row < 8][16 columns] u64
-QT_DEV size_t aohs_qcnt_off(int CG, int nk) { return aohs_gran_off(CG, nk) + (size_t)CG * nk * 8 * 32 * 8; }
-QT_DEV size_t aohs_qgran_off(int CG, int nk) {
-  return aohs_qcnt_off(CG, nk) + ((size_t)CG * nk * 8 * 4 + 255) / 256 * 256;
-}
 
-// QKV: the q/k/v projection fused in (qt_attn_oproj_args.w_qkv): block (cg, h) computes column tile cg of head h's
-// (NREP + 2) * D q/k/v columns for every row (the GEMV of a 16-column tile over K_in, RMS-normalised a16 rows, eight
-// waves splitting K), publishes it as {value, tag} granules and gathers the head's other 31 tiles; the separate q/k/v
-// GEMV launch and its round trip through memory go away.
-template <int D, int NREP, bool QKV>
+template <int D, int NREP>
 __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   const qt_attn_oproj_args& p = pk.a;
   constexpr int NW = 8, NT = 2, E = 8, KT = 32, NC = NT * 16;
@@ -984,9 +974,6 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   __shared__ float red[NW][64][4];
   __shared__ float part[NW][NC];
   __shared__ float gath[8][NC];
-  constexpr int QW = (NREP + 2) * D, QKPW = 4;  // head's q/k/v columns; k tiles of K_in per wave (K_in = 8 * 4 * 32)
-  __shared__ float qkv_s[QKV ? 8 : 1][QKV ? QW : 1];
-  __shared__ float red_ss[NW][16];
   __shared__ int fail_sh;
   const int R = p.R, nq = p.Hq, nk = p.Hkv;
   const int lg = pk.cg_log2;  // (the runtime divisions cost ~60 scalar instructions ahead of the first load)
@@ -1002,7 +989,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   const int e0 = sub * 8, ec = e0 % half;
   const int vsel = min(grp, NREP + 1);  // lane group -> q head h*NREP + grp, k head h, v head h
   const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? nq + h : nq + nk + h);
-  const float* xsrc = QKV ? p.cos_tab : p.qkv + (long long)r * nvec * D + (long long)hh * D + e0;
+  const float* xsrc = p.qkv + (long long)r * nvec * D + (long long)hh * D + e0;
   unsigned* cnt = (unsigned*)((char*)p.ws + 256);
   unsigned long long* gran = (unsigned long long*)((char*)p.ws + aohs_gran_off(CG, nk));
   const int ktiles = nq * D / KT;
@@ -1011,33 +998,11 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   // loads + explicit waits let the register allocator copy a destination before its wait -- stale data,
   // nondeterministic results; tools/asm_load_hazards.py)
   u32x4_t xq[2], nwr[2], cvr[2], svr[2];
-  // fused q/k/v: this block's weight tile (column tile cg of head h: q heads, then k, then v) and the rows' A
-  // fragments of this wave's K slice, the previous tags of the granules wave 0 publishes, this block's gather count
-  u32x4_t qa[QKV ? QKPW : 1], qw[QKV ? QKPW : 1];
-  u32x2_t qprev[QKV ? 4 : 1];
-  unsigned qcnt = 0;
-  const int qrow = (tid >> 4) & 7;  // the row of the q/k/v granules this thread gathers
-  unsigned* cntq = (unsigned*)((char*)p.ws + aohs_qcnt_off(CG, nk));
-  unsigned long long* granq = (unsigned long long*)((char*)p.ws + aohs_qgran_off(CG, nk));
-  if constexpr (QKV) {
-    const int col0 = cg < NREP * D / 16 ? h * NREP * D + cg * 16
-                                        : (cg < (NREP + 1) * D / 16 ? nq * D + h * D + (cg - NREP * D / 16) * 16
-                                                                    : (nq + nk) * D + h * D + (cg - (NREP + 1) * D / 16) * 16);
-    const int ktq = p.K_in / 32;
-    const bf16_t* wq = (const bf16_t*)p.w_qkv + ((size_t)(col0 / 16) * ktq + w * QKPW) * 512 + lane * 8;
-    const bf16_t* aq = (const bf16_t*)p.a16 + (long long)min(lm, R - 1) * p.lda16 + w * QKPW * 32 + lk * 8;
-#pragma unroll
-    for (int i = 0; i < QKPW; ++i) { qa[i] = ld_u32x4(aq + i * 32); qw[i] = ld_u32x4(wq + (size_t)i * 512); }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      qprev[i] = *(const u32x2_t*)(granq + (((size_t)h * CG + cg) * 8 + min(lk * 4 + i, 7)) * 16 + lm);
-    qcnt = ld_u32(cntq + ((size_t)cg * nk + h) * 8 + qrow);
-  }
   {
     const float* nwp = vsel < NREP ? (p.q_norm ? p.q_norm + e0 : xsrc) : (p.k_norm ? p.k_norm + e0 : xsrc);
     const float* cs = p.cos_tab + (long long)kvpos * half + ec;
     const float* sn = p.sin_tab + (long long)kvpos * half + ec;
-    if constexpr (!QKV) { xq[0] = ld_u32x4(xsrc); xq[1] = ld_u32x4(xsrc + 4); }
+    xq[0] = ld_u32x4(xsrc); xq[1] = ld_u32x4(xsrc + 4);
     nwr[0] = ld_u32x4(nwp); nwr[1] = ld_u32x4(nwp + 4);
     cvr[0] = ld_u32x4(cs); cvr[1] = ld_u32x4(cs + 4);
     svr[0] = ld_u32x4(sn); svr[1] = ld_u32x4(sn + 4);
@@ -1068,83 +1033,8 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   cprev = ld_u32(cnt + cg * nk + h);
   __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any of the phases' math
   if (pk.stop == 1) {
-    if ((kq[0][0] ^ wv[0][0] ^ gprev[0] ^ xres_u ^ cprev ^ (QKV ? qa[0][0] ^ qw[0][0] ^ qprev[0][0] ^ qcnt : xq[0][0])) ==
-        0x9E3779B9u)
-      p.x[0] = 0.f;
+    if ((xq[0][0] ^ kq[0][0] ^ wv[0][0] ^ gprev[0] ^ xres_u ^ cprev) == 0x9E3779B9u) p.x[0] = 0.f;
     return;
-  }
-  if constexpr (QKV) {
-    // 1b. q/k/v column tile: MFMA over this wave's K slice (rows >= R zero), sums of squares of the A rows (RMS),
-    // partials reduced in LDS in wave order; wave 0 scales, publishes the tile and keeps it in LDS
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < QKPW; ++i) {
-      const u32x4_t av = lm < R ? qa[i] : u32x4_t{0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const unsigned u = av[e];
-        ss = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, u), __builtin_bit_cast(bf16x2_t, u), ss, false);
-      }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av), __builtin_bit_cast(bf16x8_t, qw[i]),
-                                                    acc, 0, 0, 0);
-    }
-    ss += xor_lane<16>(ss);
-    ss += xor_lane<32>(ss);
-    red[w][lane][0] = acc[0]; red[w][lane][1] = acc[1]; red[w][lane][2] = acc[2]; red[w][lane][3] = acc[3];
-    if (lk == 0) red_ss[w][lm] = ss;
-    if (tid == 0) fail_sh = 0;
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = lk * 4 + i;
-        float v = 0.f, sr = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < NW; ++ww) { v += red[ww][lane][i]; sr += red_ss[ww][row]; }
-        const float y = v * rsqrtf(sr / (float)p.K_in + p.eps_in);
-        if (row < R) {
-          qkv_s[row][cg * 16 + lm] = y;
-          __hip_atomic_store(granq + (((size_t)h * CG + cg) * 8 + row) * 16 + lm,
-                             ((unsigned long long)(qprev[i][1] + 1u) << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    // 1c. gather head h's other column tiles: thread (tile group tid >> 7, row qrow, column tid & 15) takes tiles
-    // (tid >> 7) + 4 k, every tag = this block's count + 1
-    if (qrow < R) {
-      const unsigned want = qcnt + 1u;
-      const int c16 = tid & 15;
-      unsigned long long g[8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int ct = (tid >> 7) + 4 * kk;
-        g[kk] = __hip_atomic_load(granq + (((size_t)h * CG + ct) * 8 + qrow) * 16 + c16, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int ct = (tid >> 7) + 4 * kk;
-        if (ct == cg) continue;  // this block's own tile (in LDS already)
-        const unsigned long long* src = granq + (((size_t)h * CG + ct) * 8 + qrow) * 16 + c16;
-        int spins = 0;
-        while ((unsigned)(g[kk] >> 32) != want) {
-          if (++spins > pk.spin_limit) { fail_sh = 1; break; }
-          __builtin_amdgcn_s_sleep(1);
-          g[kk] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        qkv_s[qrow][ct * 16 + c16] = __uint_as_float((unsigned)g[kk]);
-      }
-      if (tid < 128 && c16 == 0) cntq[((size_t)cg * nk + h) * 8 + qrow] = want;
-    }
-    __syncthreads();
-    if (tid == 0 && fail_sh) atomicOr((int*)p.ws, 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      xq[0][i] = __float_as_uint(qkv_s[r][grp * D + e0 + i]);
-      xq[1][i] = __float_as_uint(qkv_s[r][grp * D + e0 + 4 + i]);
-    }
   }
 
   // 2. q/k RMSNorm + RoPE of head h's vectors of row r (v passes through), into LDS
@@ -1289,7 +1179,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
     }
     red[w][lane][0] = acc[0]; red[w][lane][1] = acc[1]; red[w][lane][2] = acc[2]; red[w][lane][3] = acc[3];
   }
-  if (!QKV && tid == 0) fail_sh = 0;
+  if (tid == 0) fail_sh = 0;
   __syncthreads();
   // 5. row w's partial (thread (w, c < NC)): the column tile's waves summed in wave order; publish it to the block of
   // head w (rows < R other than h), keep row h
@@ -1450,16 +1340,12 @@ extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
 
 extern "C" long long qt_attn_oproj_ws_bytes(int N, int Hkv) {
   const long long cg = (N + 31) / 32;
-  return 256 + (cg * Hkv * 4 + 255) / 256 * 256 + cg * Hkv * 8 * 32 * 8  // o_proj partial hand-offs
-         + (cg * Hkv * 8 * 4 + 255) / 256 * 256 + (long long)Hkv * cg * 8 * 16 * 8;  // fused q/k/v exchange
+  return 256 + (cg * Hkv * 4 + 255) / 256 * 256 + cg * Hkv * 8 * 32 * 8;
 }
 
 extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   if (!a || a->R <= 0 || a->Hkv <= 0 || a->Hkv > 8 || a->Hq % a->Hkv || a->N <= 0 || a->Lmax <= 0) return QT_ERR_SHAPE;
-  const bool fq = a->w_qkv != nullptr;  // q/k/v projection fused in (head-split form only)
-  if ((!fq && !a->qkv) || (fq && !a->a16) || !a->w_o || !a->x || !a->k_cache || !a->v_cache || !a->cos_tab ||
-      !a->sin_tab)
-    return QT_ERR_ARG;
+  if (!a->qkv || !a->w_o || !a->x || !a->k_cache || !a->v_cache || !a->cos_tab || !a->sin_tab) return QT_ERR_ARG;
   if (a->const_pos < 0 && (!a->rope_pos || !a->kv_pos || !a->row_start)) return QT_ERR_ARG;
   if (a->w_dtype != a->kv_dtype || (a->w_dtype != QT_BF16 && a->w_dtype != QT_F32)) return QT_ERR_DTYPE;
   hipStream_t s = (hipStream_t)stream;
@@ -1467,20 +1353,13 @@ extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   // head-split form: a workspace was given and the shape is the code predictor's (the caller decides by passing ws);
   // QT_AO_SPIN bounds each hand-off poll (iterations of ~1 us)
   static const int spin = [] { const char* e = getenv("QT_AO_SPIN"); return e ? atoi(e) : 200000; }();
-  const bool hs = a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
-                  a->R <= 8 && a->R <= a->Hkv && a->N % 256 == 0 && a->const_pos < a->Lmax &&  // row r's sum: head r's block
-                  a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv);
-  if (fq) {  // one 16-column q/k/v tile per (column group, kv head) block; K_in = 8 waves x 4 k tiles of 32
-    if (!hs || a->N / 32 != (a->Hq / a->Hkv + 2) * a->D / 16 || a->K_in != 1024 || a->a16 == a->x16 ||
-        a->lda16 < a->K_in)
-      return QT_ERR_SHAPE;
-  }
-  if (hs) {
+  if (a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
+      a->R <= 8 && a->R <= a->Hkv && a->N % 256 == 0 && a->const_pos < a->Lmax &&  // row r's sum: head r's block
+      a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv)) {
     static const int stop = [] { const char* e = getenv("QT_AO_STOP"); return e ? atoi(e) : 0; }();
     const int cgs = a->N / 32;
     const int lg = (cgs & (cgs - 1)) == 0 ? __builtin_ctz((unsigned)cgs) : -1;
-    if (fq) hipLaunchKernelGGL((attn_oproj_hs_k<128, 2, true>), dim3(cgs * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop, lg});
-    else hipLaunchKernelGGL((attn_oproj_hs_k<128, 2, false>), dim3(cgs * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop, lg});
+    hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(cgs * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop, lg});
     return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
   }
   switch (a->D) {

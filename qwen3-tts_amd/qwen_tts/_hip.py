@@ -67,8 +67,7 @@ class AttnOprojArgs(ctypes.Structure):
                 ("rope_pos", c_void_p), ("kv_pos", c_void_p), ("row_start", c_void_p), ("const_pos", c_int),
                 ("k_cache", c_void_p), ("v_cache", c_void_p), ("kv_dtype", c_int), ("w_o", c_void_p), ("w_dtype", c_int),
                 ("N", c_int), ("x", c_void_p), ("ldx", c_ll), ("x16", c_void_p), ("ldx16", c_ll), ("ws", c_void_p),
-                ("ws_bytes", c_ll), ("a16", c_void_p), ("lda16", c_ll), ("w_qkv", c_void_p), ("K_in", c_int),
-                ("eps_in", c_float)]
+                ("ws_bytes", c_ll)]
 
 
 class SampleArgs(ctypes.Structure):

@@ -259,13 +259,10 @@ def attn_oproj_ws_bytes(N, Hkv):
 
 
 def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc, Lmax, w_o: "Tiled", x, *,
-                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None, x16=None, ws=None, a16=None,
-                      w_qkv: "Tiled" = None, eps_in=1e-6):
+                      const_pos=-1, rope_pos=None, kv_pos=None, row_start=None, x16=None, ws=None):
     """qt_decode_attn_oproj: x[:R] += o_proj(decode attention) in one launch (row r = batch entry r, short caches).
     x16: bf16 shadow of x, updated alongside.  ws: zeroed uint8 scratch of attn_oproj_ws_bytes(N, Hkv), private to
-    one stream -- enables the head-split form (its int32 word 0 is the sticky hand-off error flag).
-    a16 + w_qkv (head-split form): the q/k/v projection fused in -- q/k/v = rms(a16) @ w_qkv (qkv is not read);
-    a16 must be a different buffer from x16."""
+    one stream -- enables the head-split form (its int32 word 0 is the sticky hand-off error flag)."""
     a = _hip.AttnOprojArgs()
     a.R, a.Hq, a.Hkv, a.D, a.Lmax = R, Hq, Hkv, D, Lmax
     a.qkv, a.q_norm, a.k_norm, a.eps = ptr(qkv), ptr(q_norm), ptr(k_norm), eps
@@ -278,8 +275,6 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
         a.x16, a.ldx16 = ptr(x16), x16.stride(0)
     if ws is not None:
         a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
-    if w_qkv is not None:
-        a.a16, a.lda16, a.w_qkv, a.K_in, a.eps_in = ptr(a16), a16.stride(0), ptr(w_qkv.w), w_qkv.K, eps_in
     check(_hip.lib().qt_decode_attn_oproj(ctypes.byref(a), stream()), "qt_decode_attn_oproj")
 
 

@@ -91,20 +91,8 @@ class _Stack:
         if x16 is not None and R > 96 and not PF:
             x16 = None  # igemm_k writes x only (decode / skinny GEMVs and gemm_pf_k keep the shadow)
         xa = x if x16 is None else x16
-        x16b = (scratch.get("x16b") if fused_ao and x16 is not None and R <= min(8, self.Hkv) and "ao_ws" in scratch
-                else None)
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            xm = xa  # the gate/up GEMV's A operand
-            if x16b is not None and not (qkv0 and li == 0):
-                # q/k/v projection + attention + o_proj + residual in one launch: reads the shadow x16 (written by the
-                # previous down GEMV), writes x and the second shadow x16b, which the gate/up GEMV reads
-                K.decode_attn_oproj(None, R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps, self.cos,
-                                    self.sin, kc, vc, Lmax, L.o, x, const_pos=meta["const_pos"], x16=x16b,
-                                    ws=scratch["ao_ws"], a16=x16, w_qkv=L.qkv, eps_in=self.eps)
-                K.gemm(x16b, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
-                K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD, out2=x16)
-                continue
             if not (qkv0 and li == 0):
                 K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
@@ -127,7 +115,7 @@ class _Stack:
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
             if not fused_ao:
                 K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD, out2=x16)
-            K.gemm(xm, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
+            K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
             K.gemm(scratch["h"], L.down, x, R, self.I, self.H, epi=_hip.EPI_ADD, out2=x16)
 
 
@@ -144,9 +132,6 @@ ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
 # less L2 -> CU traffic than the (column group, row) form (profiles/r04_pmc_attn_oproj*.json), 7.71 -> 7.03 us per
 # launch, bench 200.2 -> 202.8 audio-s/s (profiles/r04_bench_ab_ao_hs.txt).  QT_AO_HS=0 keeps the other form (A/B)
 AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
-# ... with the q/k/v projection fused in as well (decode steps past layer 0, whose q/k/v come from the tables): one
-# launch instead of the q/k/v GEMV + the fused attention; QT_AO_QKV=0 keeps the two launches (A/B)
-AO_QKV = os.environ.get("QT_AO_QKV", "0") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -202,16 +187,7 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     sc["attn_oproj"] = attn_oproj and ATTN_OPROJ and _attn_oproj_ok(st)
     if sc["attn_oproj"] and AO_HS:  # hand-off granules + sequence counters of the head-split form (zeroed once)
         sc["ao_ws"] = torch.zeros(K.attn_oproj_ws_bytes(st.H, st.Hkv), dtype=torch.uint8, device=dev)
-        if AO_QKV and _ao_qkv_ok(st):  # second bf16 residual shadow: the fused q/k/v launch reads one, writes the other
-            sc["x16b"] = torch.zeros(R, st.H, dtype=torch.bfloat16, device=dev)
     return sc
-
-
-def _ao_qkv_ok(st: _Stack) -> bool:
-    """Shapes the fused q/k/v + attention + o_proj launch takes (qt_decode_attn_oproj with w_qkv): one 16-column q/k/v
-    tile per (32-column output group, kv head) block, K = 1024 split over 8 waves."""
-    return (st.wdt == torch.bfloat16 and st.D == 128 and st.Hq == 2 * st.Hkv and st.H == 1024
-            and st.H // 32 == (st.Hq // st.Hkv + 2) * st.D // 16)
 
 
 def check_handoffs(sessions):

@@ -71,24 +71,7 @@ def main():
     timed(chain2, "chain qkv -> attn -> o_proj (per 3 launches)")
     timed(chain1, "chain qkv -> fused (per 2 launches)")
     timed(chain1h, "chain qkv -> fused head-split (per 2 launches)")
-    # the engine's bf16-shadow form: the q/k/v GEMV reads x16, the fused launch writes it; and the q/k/v projection
-    # fused into the head-split launch (reads x16a, writes x16b)
-    x16a, x16b = x.to(dt), torch.zeros(B, H, device=dev, dtype=dt)
-    ws2 = torch.zeros(K.attn_oproj_ws_bytes(H, hkv), dtype=torch.uint8, device=dev)
-
-    def chain1h16():
-        i = nxt()
-        K.gemm(x16a, qkv_w[i], qkv, B, H, (hq + 2 * hkv) * D, rms=True, eps=1e-6)
-        K.decode_attn_oproj(qkv, B, hq, hkv, D, qn, qn, 1e-6, cos, sin, kc[i], vc[i], L + 1, o_w[i], x,
-                            const_pos=L - 1, ws=ws, x16=x16a)
-
-    def fused_qkv():
-        i = nxt()
-        K.decode_attn_oproj(None, B, hq, hkv, D, qn, qn, 1e-6, cos, sin, kc[i], vc[i], L + 1, o_w[i], x,
-                            const_pos=L - 1, ws=ws2, x16=x16b, a16=x16a, w_qkv=qkv_w[i], eps_in=1e-6)
-    timed(chain1h16, "chain qkv(x16) -> fused head-split (per 2 launches)")
-    timed(fused_qkv, "fused q/k/v + attention + o_proj (one launch)")
-    print("hand-off error flag", int(ws[:4].view(torch.int32).item()), int(ws2[:4].view(torch.int32).item()))
+    print("hand-off error flag", int(ws[:4].view(torch.int32).item()))
 
 
 if __name__ == "__main__":
