@@ -1,4 +1,4 @@
-# Round-4 end measurement on the current build: PMC passes (attn_oproj_hs_k: the bench's roofline kernel, and the
+# Round-4 end measurement (final build) on the current build: PMC passes (attn_oproj_hs_k: the bench's roofline kernel, and the
 # talker gate-up GEMV), copied into profiles/ on the box so the bench line's traffic is this build's, then the bench
 # line and the rocprofv3 kernel-trace stats of the same bench command.  Each GPU step time-limited, chained (set -e).
 set -e
@@ -9,12 +9,12 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_R
   d=gpurun_out/pmc_ao_$(echo $pass | tr ' ' '_')
   timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d $d -o run -- python3 tools/pmc_attn_oproj.py > $d.log 2>&1
 done
-python3 tools/pmc_kernel_reduce.py attn_oproj_hs_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04b_pmc_attn_oproj_hs.json
-python3 tools/pmc_kernel_reduce.py attn_oproj_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04b_pmc_attn_oproj.json
+python3 tools/pmc_kernel_reduce.py attn_oproj_hs_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04c_pmc_attn_oproj_hs.json
+python3 tools/pmc_kernel_reduce.py attn_oproj_k gpurun_out/pmc_ao_meta.txt gpurun_out/pmc_ao_* > gpurun_out/r04c_pmc_attn_oproj.json
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc1 -o run -- python3 tools/pmc_gateup.py > gpurun_out/pmc1.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc2 -o run -- python3 tools/pmc_gateup.py > gpurun_out/pmc2.log 2>&1
-python3 tools/pmc_reduce.py gpurun_out/pmc1 gpurun_out/pmc2 "$(cat gpurun_out/pmc_build_id.txt)" > gpurun_out/r04b_pmc_gateup.json
-cp gpurun_out/r04b_pmc_*.json profiles/
-timeout -k 10 600 python bench.py > gpurun_out/r04b_bench.log 2>&1
-tail -1 gpurun_out/r04b_bench.log > gpurun_out/r04b_bench_line.json
-bash tools/prof.sh r04bprof --cpu-baseline 0
+python3 tools/pmc_reduce.py gpurun_out/pmc1 gpurun_out/pmc2 "$(cat gpurun_out/pmc_build_id.txt)" > gpurun_out/r04c_pmc_gateup.json
+cp gpurun_out/r04c_pmc_*.json profiles/
+timeout -k 10 600 python bench.py > gpurun_out/r04c_bench.log 2>&1
+tail -1 gpurun_out/r04c_bench.log > gpurun_out/r04c_bench_line.json
+bash tools/prof.sh r04cprof --cpu-baseline 0
