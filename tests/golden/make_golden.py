@@ -326,12 +326,12 @@ class _TeacherForcer:
 def make_full_bf16(only=None):
     """The reference itself in bf16 (the examples' dtype, examples/test_model_12hz_custom_voice.py:30: parameters cast to
     bf16 as from_pretrained(dtype=torch.bfloat16) loads them; buffers such as RoPE inv_freq stay fp32), eager CPU, on
-    the full-dim cases cv17_b8_stream and cv06_b1_nonstream: (1) teacher-forced on the fp32 reference codes of
+    the full-dim cases cv17_b8_stream, cv06_b1_nonstream and cv17_b2_long (256 frames): (1) teacher-forced on the fp32 reference codes of
     full_<key>.npz -- its own greedy pick at every position; (2) free-running greedy codes.  Written to
     full_<key>_refbf16.npz: the calibration of bf16 agreement (tests/test_gpu_full.py)."""
     import transformers.generation.logits_process as lp
     from cases import full_cases
-    for key in ("cv17_b8_stream", "cv06_b1_nonstream"):
+    for key in ("cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long"):
         if only and key != only:
             continue
         case = full_cases()[key]

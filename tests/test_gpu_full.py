@@ -41,7 +41,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TOL_FP32 = 1e-4   # |fp32 GPU - fp32 CPU| logit differences measured here are < 1e-5
-REF_BF16 = ["cv17_b8_stream", "cv06_b1_nonstream"]  # cases with a reference-bf16 fixture
+REF_BF16 = ["cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long"]  # cases with a reference-bf16 fixture
 
 
 def _ref_bf16_flip_margin():
@@ -59,7 +59,7 @@ def _ref_bf16_flip_margin():
     return float(np.nextafter(np.float32(worst), np.float32(np.inf)))  # strict bound: flips AT that margin pass
 
 
-TOL_BF16 = _ref_bf16_flip_margin()  # 0.0683 (cv17: 230 flips, cv06: 48, max 0.0454): measured on the reference
+TOL_BF16 = _ref_bf16_flip_margin()  # 0.0803 with the 256-frame case (0.0683 on cv17 / cv06): measured on the reference
 
 
 def _dev():
