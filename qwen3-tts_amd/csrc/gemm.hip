@@ -999,11 +999,6 @@ int launch(const GemmP& p, hipStream_t s) {
   const int nt = (p.N + 15) / 16;
   constexpr int KT = sizeof(WT) == 2 ? 32 : 16;
   if constexpr (sizeof(WT) == 2 && sizeof(AT) == 2) {
-    if (p.sk == 2) {
-      if constexpr (std::is_same<OT, float>::value) qt_gemm_impl::launch_sk2_f32(p, s);
-      else qt_gemm_impl::launch_sk2_bf16(p, s);
-      return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
-    }
     if (p.sk) {
       if constexpr (std::is_same<OT, float>::value) qt_gemm_impl::launch_sk_f32(p, s);
       else qt_gemm_impl::launch_sk_bf16(p, s);
@@ -1248,21 +1243,11 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   p.sk = 0;
   p.pf_small = 0;
   static const int skinny_env = [] { const char* e = getenv("QT_SKINNY"); return e ? atoi(e) : 1; }();
-  bool skinny = skinny_env != 0 && a->M > 16 && a->M <= 256 && a->taps == 0 && a->w_dtype == QT_BF16 &&
+  const bool skinny = skinny_env != 0 && a->M > 16 && a->M <= 256 && a->taps == 0 && a->w_dtype == QT_BF16 &&
                       a->a_dtype == QT_BF16 && a->K % 64 == 0 && a->a_index == nullptr && a->gamma == nullptr &&
                       a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr && a->lda % 8 == 0 &&
                       ((size_t)a->A & 15) == 0 && a->N >= 32;
   bool skinny_gemv = false;
-  // gemm_sk2_k (QT_SK2=1, A/B): 49..128 rows, K % 512 == 0, K <= 4096, split records in ws
-  static const int sk2_env = [] { const char* e = getenv("QT_SK2"); return e ? atoi(e) : 0; }();
-  if (skinny && sk2_env && a->M > 48 && a->M <= 128 && a->K % 512 == 0 && a->K <= 4096 && a->N % 64 == 0 &&
-      a->ws && a->ws_bytes >= 4096 * (long long)sizeof(unsigned) + qt_gemm_impl::sk2_part_bytes(a->M, a->N, a->K) &&
-      (a->N + 63) / 64 <= 4096) {
-    p.sk = 2;
-    p.cnt = (unsigned*)a->ws;
-    p.part = (float*)((char*)a->ws + 4096 * sizeof(unsigned));
-    skinny = false;
-  }
   if (skinny) {
     if (a->N >= 4096) {
       if (a->M <= sk_max_m() && (long long)a->N * a->K <= (8ll << 20)) p.sk = 1;

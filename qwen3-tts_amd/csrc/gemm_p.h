@@ -25,7 +25,7 @@ struct GemmP {
   int a_elu;                    // ELU on A (tokenizer encoder convs)
   int mr;                       // decode GEMV rows per row group (gridDim.z = ceil(M / mr))
   bf16_t* out2; long long ldo2; // optional bf16 copy of the stored output (decode residual stream shadow)
-  int sk;                       // 1: skinny GEMM (gemm_sk_k, 17..64 rows, every row in one block); 2: gemm_sk2_k
+  int sk;                       // 1: skinny GEMM (gemm_sk_k, 17..64 rows, every row in one block)
   int pf_small;                 // 1: gemm_pf2_k below its default row floor (17..256-row routing in qt_gemm)
 };
 
@@ -35,9 +35,5 @@ void launch_pf2_auto_bf16(const GemmP& p, hipStream_t s);
 // gemm_sk_k (gemm_sk.hip): 17..64 rows, bf16 A and bf16 pre-tiled W, K % 32 == 0, 16-byte aligned A rows
 void launch_sk_f32(const GemmP& p, hipStream_t s);
 void launch_sk_bf16(const GemmP& p, hipStream_t s);
-// gemm_sk2_k (gemm_sk.hip): 49..128 rows, K % 512 == 0 (<= 4096), 64-column blocks x 512-deep K splits (p.ks = sk == 2)
-void launch_sk2_f32(const GemmP& p, hipStream_t s);
-void launch_sk2_bf16(const GemmP& p, hipStream_t s);
-long long sk2_part_bytes(int M, int N, int K);  // split records in p.part
 
 }  // namespace qt_gemm_impl
