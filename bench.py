@@ -210,6 +210,21 @@ def _pmc_traffic(tag):
 PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj"}
 
 
+def _rocprof_avg(tag):
+    """Average kernel duration (us, begin -> end) of a kernel in the rocprofv3 --kernel-trace --stats run of this bench
+    command committed for this library's build (profiles/*_rocprof_<tag>.json, reduced from the stats CSV by
+    tools/rocprof_kernel_avg.py).  The bench's own per-launch time is a graph replay of dependent launches divided by
+    the launches, so it also holds the dispatch gap between them; the two are reported side by side."""
+    from qwen_tts import _hip
+    pdir = os.path.join(REPO, "profiles")
+    for f in sorted(os.listdir(pdir), reverse=True):
+        if f.endswith(f"_rocprof_{tag}.json"):
+            j = json.load(open(os.path.join(pdir, f)))
+            if j.get("build_id") == _hip.BUILD_ID:
+                return j.get("avg_us"), f"profiles/{f} (this build, {j['build_id']}, {j.get('calls')} launches)"
+    return None, None
+
+
 def whole_frame_roofline(tts, cfg, B, reps=32):
     """The captured per-frame graph (15 code-predictor steps + the talker step + token choices) of the bench's own
     session replayed `reps` times at its final cache length: algorithmic bytes per frame / time per frame."""
@@ -454,11 +469,14 @@ def main():
         def as_roof(e):
             tag = e.get("pmc_tag", PMC_TAG.get(e["name"]))
             traffic, tsrc = _pmc_traffic(tag) if tag else (None, None)
+            rp_us, rp_src = _rocprof_avg(tag) if tag else (None, None)
             return {"bound": e["bound"], "kernel": e["kernel"], "achieved": round(e["gbs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(e["frac"], 4), "traffic": traffic, "traffic_source": tsrc,
                     "avg_launch_us": round(e["avg_us"], 2), "bytes_per_launch": int(e["bytes"]),
                     "launches_per_frame": e["launches_per_frame"], "us_per_frame": round(e["us_per_frame"], 1),
-                    "frame_share": None if frame_us is None else round(e["us_per_frame"] / frame_us, 4)}
+                    "frame_share": None if frame_us is None else round(e["us_per_frame"] / frame_us, 4),
+                    "rocprof_avg_us": rp_us, "rocprof_source": rp_src,
+                    "achieved_at_rocprof_avg": None if not rp_us else round(e["bytes"] / (rp_us * 1e-6) / 1e9, 1)}
         # the dominant decode kernel = the largest measured time per frame (launch time x launches per frame)
         dom = max(tab, key=lambda e: e["us_per_frame"])
         roof = dict(as_roof(dom), selected_by="largest measured time per frame among the decode kernels (kernel_table)")

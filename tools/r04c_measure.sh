@@ -18,3 +18,7 @@ cp gpurun_out/r04c_pmc_*.json profiles/
 timeout -k 10 600 python bench.py > gpurun_out/r04c_bench.log 2>&1
 tail -1 gpurun_out/r04c_bench.log > gpurun_out/r04c_bench_line.json
 bash tools/prof.sh r04cprof --cpu-baseline 0
+# the roofline kernels' average durations in that trace, labelled with the build (bench.py attaches them by build id)
+bid=$(cat gpurun_out/pmc_build_id.txt)
+python3 tools/rocprof_kernel_avg.py gpurun_out/r04cprof/run_kernel_stats.csv attn_oproj_hs_k $bid > gpurun_out/r04c_rocprof_attn_oproj_hs.json
+python3 tools/rocprof_kernel_avg.py gpurun_out/r04cprof/run_kernel_stats.csv "gemv_wt<unsigned short, unsigned short, unsigned short, 4, 4, true, true" $bid > gpurun_out/r04c_rocprof_gateup.json
