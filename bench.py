@@ -4,6 +4,9 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N` (N > 1) without a launcher starts the N ranks itself (torch.distributed.run in a child process, before
+this process makes any GPU call); under a launcher WORLD_SIZE must equal N.  Ranks talk over RCCL ("nccl").
+
 One step = prefill + 256 AR frames (talker + 15-step code predictor per frame, HIP-graph replay) +
 12 Hz codec decode of all 8 utterances to 24 kHz PCM.  Weak scaling: every rank serves its own batch of
 8 independent utterances (data parallel, no collective on the data path; RCCL only broadcasts the
@@ -346,6 +349,99 @@ def cpu_baseline(B, prompt, frames, threads):
                        f"torch.set_num_threads({threads})")
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(gpus: int) -> int:
+    """`bench.py --gpus N` (N > 1) run without a torch.distributed launcher around it: start the N ranks ourselves, one
+    process per GPU, as `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py ...` in a
+    CHILD process, and return its exit code.  This process never touches the GPU (no HIP call before or after: a
+    process that has initialised the GPU must not be replaced by another), and the ranks print the one JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, QT_BENCH_LAUNCHER="self")
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(a):
+    """Rank environment of this process: (world, rank, local, backend, dist module or None, device).  Under a launcher
+    the world size must equal --gpus (the driver's 1 -> 8 scaling run passes both; a mismatch would report one GPU's
+    work as N GPUs').  QT_BENCH_BACKEND=gloo + QT_BENCH_SAME_DEVICE=1 rehearse the N > 1 path on one GPU;
+    QT_BENCH_DRYRUN=1 (CPU tests of this launcher) runs no model and no GPU at all."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} ranks were launched")
+    backend = os.environ.get("QT_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
+    dry = os.environ.get("QT_BENCH_DRYRUN") == "1"
+    if dry:
+        backend = "gloo"
+        dev = torch.device("cpu")
+    else:
+        if os.environ.get("QT_BENCH_SAME_DEVICE") == "1":
+            local = 0
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
+    return world, rank, local, backend, dist, dev
+
+
+def gather_rank_rates(dist, audio, dt):
+    """Per-rank audio-seconds/sec (rank order) -- reported beside the whole-job value."""
+    if dist is None:
+        return [audio / dt]
+    objs = [None] * dist.get_world_size()
+    dist.all_gather_object(objs, (audio, dt))
+    return [a_ / d_ for a_, d_ in objs]
+
+
+def main_dryrun(a, world, rank, dist, dev, backend):
+    """CPU rehearsal of the launcher, barriers and reductions (QT_BENCH_DRYRUN=1): every step "generates" B x frames
+    of audio in a fixed sleep.  Same JSON keys as the real line; never used for a reported number."""
+    B = a.batch
+    audio_per_step = B * a.frames * 1920 / 24000.0
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+    for _ in range(a.warmup):
+        time.sleep(0.01)
+    barrier()
+    t0 = time.perf_counter()
+    audio = 0.0
+    for _ in range(a.steps):
+        time.sleep(0.02)
+        audio += audio_per_step
+    barrier()
+    dt = time.perf_counter() - t0
+    per_rank = gather_rank_rates(dist, audio, dt)
+    if dist is not None:
+        from qwen_tts.dp import reduce_timing
+        dt, audio = reduce_timing(dt, audio, device=dev)
+    if rank == 0:
+        print(json.dumps({"metric": "dryrun", "value": round(audio / dt, 3), "unit": "audio-seconds/sec",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "dist_backend": backend if world > 1
+                          else None, "rccl_ranks": world if backend == "nccl" and world > 1 else 0,
+                          "per_rank_value": [round(v, 3) for v in per_rank], "audio_seconds": audio,
+                          "launcher": os.environ.get("QT_BENCH_LAUNCHER", "external" if world > 1 else None)}),
+              flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -364,25 +460,13 @@ def main():
                          "configs[3] (strong scaling: 64 mixed-length VoiceDesign requests LPT-sharded over the ranks)")
     ap.add_argument("--slots", type=int, default=64, help="vd64: continuously refilled batch rows per GPU")
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(a.gpus))  # before any GPU call: the N ranks run in child processes
+    world, rank, local, backend, dist, dev = init_ranks(a)
+    if os.environ.get("QT_BENCH_DRYRUN") == "1":
+        return main_dryrun(a, world, rank, dist, dev, backend)
     if a.workload == "vd64":
-        return main_vd64(a)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # test-only overrides: rehearse the N>1 path on one GPU (all ranks on cuda:0, gloo collectives)
-    backend = os.environ.get("QT_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
-    if os.environ.get("QT_BENCH_SAME_DEVICE") == "1":
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        return main_vd64(a, world, rank, dist, dev, backend)
 
     from qwen_tts import Qwen3TTSModel
     cfg, W, CW = make_weights(a.preset, dev, world, rank)
@@ -423,6 +507,7 @@ def main():
         lat.append(s_t)
     barrier()
     dt = time.perf_counter() - t0
+    per_rank = gather_rank_rates(dist, audio, dt)
     if dist is not None:
         from qwen_tts.dp import reduce_timing
         dt, audio = reduce_timing(dt, audio, device=dev)
@@ -513,7 +598,11 @@ def main():
                "first_packet_p50_ms": round(fp[B], 1), "first_packet_p50_ms_b1": round(fp[1], 1),
                "full_batch_latency_p50_ms": round(1e3 * float(np.median(lat)), 1),
                "roofline": roof, "frame_roofline": frame_roof, "kernel_table": table, "gateup_roofline": gateup,
-               "prefill_mfma": pf_roof, "cpu_baseline": cpu, "build_id": _hip.BUILD_ID}
+               "prefill_mfma": pf_roof, "cpu_baseline": cpu, "build_id": _hip.BUILD_ID,
+               "dist_backend": backend if world > 1 else None,
+               "rccl_ranks": world if backend == "nccl" and world > 1 else 0,
+               "per_rank_value": [round(v, 3) for v in per_rank],
+               "launcher": os.environ.get("QT_BENCH_LAUNCHER", "external" if world > 1 else None)}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -536,23 +625,10 @@ def vd64_requests(n=64, seed=4321):
     return ids, ins_ids, langs, [int(f) for f in frames]
 
 
-def main_vd64(a):
+def main_vd64(a, world, rank, dist, dev, backend):
     """configs[3]: one step = all 64 requests generated (sampling, exact frame counts) and decoded to PCM.  Each rank
     decodes its longest-first share (qwen_tts.dp.dp_generate: continuous batching through --slots rows, its own PCM);
     value = total audio seconds of the 64 / max-over-ranks wall time (strong scaling)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = 0 if os.environ.get("QT_BENCH_SAME_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        backend = os.environ.get("QT_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
     from qwen_tts import Qwen3TTSModel, _hip
     from qwen_tts.dp import dp_generate
     preset = "1.7b-voicedesign"
@@ -589,6 +665,7 @@ def main_vd64(a):
         audio += step(i)[0]
     barrier()
     dt = time.perf_counter() - t0
+    per_rank = gather_rank_rates(dist, audio, dt)
     if dist is not None:
         from qwen_tts.dp import reduce_timing
         dt, audio = reduce_timing(dt, audio, device=dev)
@@ -603,7 +680,10 @@ def main_vd64(a):
                                       "instruct U[10,60] tokens, F U[64,320] frames, sampling) LPT-sharded over the "
                                       f"ranks, {a.slots} refilled rows per GPU, + codec decode",
                           "global_batch": 64, "frames_total": int(sum(frames)), "parallelism": f"dp{world}"},
-               "build_id": _hip.BUILD_ID}
+               "build_id": _hip.BUILD_ID, "dist_backend": backend if world > 1 else None,
+               "rccl_ranks": world if backend == "nccl" and world > 1 else 0,
+               "per_rank_value": [round(v, 3) for v in per_rank],
+               "launcher": os.environ.get("QT_BENCH_LAUNCHER", "external" if world > 1 else None)}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

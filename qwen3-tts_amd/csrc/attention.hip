@@ -701,7 +701,7 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
   asm_ld4(xres_u, p.x + (long long)r * p.ldx + min(cg * NT * 16 + (lane % (NT * 16)), p.N - 1));
   constexpr int N_W = NT * KTS + 1;  // loads younger than the cached keys (weights + residual)
   constexpr int N_KV = 2 * IC * RQ;
-  if (pk.stop == 1) {
+  if (kProbe && pk.stop == 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     reg_fence(xres_u); reg_fence(kq[0][0]); reg_fence(wv[0][0]);
     if ((kq[0][0][0] ^ wv[0][0][0]) == 0x9E3779B9u && xres_u == 7u) p.x[0] = 0.f;
@@ -762,7 +762,7 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
     }
   }
   __syncthreads();
-  if (pk.stop == 2) {
+  if (kProbe && pk.stop == 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     reg_fence(kq[0][0]); reg_fence(wv[0][0]);
     if (qs[0][lane] == 1234.5f && kq[0][0][0] == 7u && wv[0][0][0] == 7u) p.x[0] = 0.f;
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
     gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = from_f<AT>(ov / lv); });
   }
   __syncthreads();
-  if (pk.stop == 3) {
+  if (kProbe && pk.stop == 3) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (to_f(att[w][lane]) == 1234.5f) p.x[0] = 0.f;
     return;
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(512) void attn_oproj_k(AOK pk) {
     }
   }
   __syncthreads();
-  if (pk.stop == 4) {
+  if (kProbe && pk.stop == 4) {
     if (red[0][0][lane & 15] == 1234.5f) p.x[0] = 0.f;
     return;
   }
@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
   xres_u = ld_u32(p.x + (long long)min(h, R - 1) * p.ldx + cg * NC + (lane & (NC - 1)));
   cprev = ld_u32(cnt + cg * nk + h);
   __builtin_amdgcn_sched_barrier(0);  // every load above is issued before any of the phases' math
-  if (pk.stop == 1) {
+  if (kProbe && pk.stop == 1) {
     if ((xq[0][0] ^ kq[0][0] ^ wv[0][0] ^ gprev[0] ^ xres_u ^ cprev) == 0x9E3779B9u) p.x[0] = 0.f;
     return;
   }
@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
     }
   }
   __syncthreads();
-  if (pk.stop == 2) {
+  if (kProbe && pk.stop == 2) {
     if (qs2[w][0][lane] == 12345u && kq[0][0] == 7u && wv[0][0] == 7u) p.x[0] = 0.f;
     return;
   }
@@ -1161,7 +1161,7 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
     gm.each(lane, [&](int j, int d, float ov, float lv, float) { att[w][j * D + d] = f2bf(ov * __builtin_amdgcn_rcpf(lv)); });
   }
   __syncthreads();
-  if (pk.stop == 3) {
+  if (kProbe && pk.stop == 3) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (bf2f(att[w][lane]) == 1234.5f) p.x[0] = 0.f;
     return;
@@ -1189,13 +1189,13 @@ __global__ __launch_bounds__(512) void attn_oproj_hs_k(AOHS pk) {
 #pragma unroll
     for (int q2 = 0; q2 < WPT; ++q2) v += red[t * WPT + q2][(w >> 2) * 16 + cc][w & 3];
     part[w][c] = v;
-    if (pk.stop == 4) {
+    if (kProbe && pk.stop == 4) {
       if (v == 1234.5f) p.x[0] = 0.f;
     } else if (w < R && w != h)
       __hip_atomic_store(gran + my_g, ((unsigned long long)(gprev[1] + 1u) << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (pk.stop == 4) return;
+  if (kProbe && pk.stop == 4) return;
   // 6. block of head h < R: the other heads' partials of row h, then the row
   if (h < R) {
     const unsigned want = cprev + 1u;
@@ -1241,7 +1241,7 @@ int attn_oproj_go(const qt_attn_oproj_args& a, hipStream_t s) {
   if constexpr ((NREP * D) % KT != 0 || (NREP * D) / KT > 16) {
     return QT_ERR_SHAPE;
   } else {
-    static const int stop = [] { const char* e = getenv("QT_AO_STOP"); return e ? atoi(e) : 0; }();
+    static const int stop = qt_knob("QT_AO_STOP", 0);
     if (a.Hq + 2 * a.Hkv > 8 * (64 / (D / 8))) return QT_ERR_SHAPE;  // one q/k/v vector per lane group
     const int cgs = ((a.N + 15) / 16 + NT - 1) / NT;
     hipLaunchKernelGGL((attn_oproj_k<WT, WT, D, NREP, NT, CPOS>), dim3(cgs * a.R), dim3(512), 0, s, AOK{a, stop});
@@ -1280,7 +1280,7 @@ int decode_dispatch(const qt_decode_attn_args& a, hipStream_t s) {
   if (ns > 1 && (!a.ws || a.ws_bytes < qt_decode_attn_ws_bytes(a.R, a.Hq, a.Hkv, a.D, ns))) return QT_ERR_ARG;
   if (ns > 1 && a.R * a.Hkv > 1024) return QT_ERR_SHAPE;  // arrival counters live in the 4 KiB header
   dim3 g(a.R, a.Hkv, ns);
-  static const int nw_env = [] { const char* e = getenv("QT_ATTN_SHORT"); return e ? atoi(e) : -1; }();
+  static const int nw_env = qt_knob("QT_ATTN_SHORT", -1);
   const bool short_cache = nw_env >= 0 ? nw_env != 0 : a.Lmax <= 64;  // 4 waves cover <= 64 keys in one pass
   switch (a.Hq / a.Hkv) {
     case 1:
@@ -1338,6 +1338,33 @@ extern "C" int qt_decode_attention(const qt_decode_attn_args* a, void* stream) {
   }
 }
 
+// The head-split form's consumers spin on granules that other blocks of the SAME launch publish, so every block of the
+// grid must be resident at once (HIP does not schedule a waiting block out).  Checked against the occupancy of this
+// kernel on the current device (cached per device): a smaller GPU / compute partition takes the (column group, row)
+// form instead, which has no in-launch hand-off.
+static bool aohs_all_resident(int blocks) {
+  static int cap[64];  // resident blocks per device, 0 = not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)attn_oproj_hs_k<128, 2>, 512, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+    cap[dev] = std::max(1, per_cu * cus);
+  }
+  return blocks <= cap[dev];
+}
+
+extern "C" int qt_attn_oproj_resident_blocks() {
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)attn_oproj_hs_k<128, 2>, 512, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  return per_cu * cus;
+}
+
 extern "C" long long qt_attn_oproj_ws_bytes(int N, int Hkv) {
   const long long cg = (N + 31) / 32;
   return 256 + (cg * Hkv * 4 + 255) / 256 * 256 + cg * Hkv * 8 * 32 * 8;
@@ -1351,12 +1378,12 @@ extern "C" int qt_decode_attn_oproj(const qt_attn_oproj_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool bf = a->w_dtype == QT_BF16;
   // head-split form: a workspace was given and the shape is the code predictor's (the caller decides by passing ws);
-  // QT_AO_SPIN bounds each hand-off poll (iterations of ~1 us)
-  static const int spin = [] { const char* e = getenv("QT_AO_SPIN"); return e ? atoi(e) : 200000; }();
+  // QT_AO_SPIN (probe builds) bounds each hand-off poll (iterations of ~1 us), never below 1000
+  static const int spin = std::max(1000, qt_knob("QT_AO_SPIN", 200000));
   if (a->ws && bf && a->const_pos >= 0 && a->const_pos <= 16 && a->D == 128 && a->Hq == 2 * a->Hkv &&
       a->R <= 8 && a->R <= a->Hkv && a->N % 256 == 0 && a->const_pos < a->Lmax &&  // row r's sum: head r's block
-      a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv)) {
-    static const int stop = [] { const char* e = getenv("QT_AO_STOP"); return e ? atoi(e) : 0; }();
+      a->ws_bytes >= qt_attn_oproj_ws_bytes(a->N, a->Hkv) && aohs_all_resident((a->N / 32) * a->Hkv)) {
+    static const int stop = qt_knob("QT_AO_STOP", 0);
     const int cgs = a->N / 32;
     const int lg = (cgs & (cgs - 1)) == 0 ? __builtin_ctz((unsigned)cgs) : -1;
     hipLaunchKernelGGL((attn_oproj_hs_k<128, 2>), dim3(cgs * a->Hkv), dim3(512), 0, s, AOHS{*a, spin, stop, lg});

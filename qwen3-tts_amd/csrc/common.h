@@ -12,6 +12,23 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
 #define QT_DEV __device__ __forceinline__
 
+// Measurement knobs of the A/B tools (tools/*.sh): read from the environment only by a probe build
+// (`build.py --probe` defines QT_PROBE_BUILD and links lib/libqwen3tts_amd_probe.so).  The product library takes the
+// compiled-in defaults: no environment-dependent routing, and the phase early exits (kProbe) are compiled out of
+// its kernels.
+#ifdef QT_PROBE_BUILD
+#include <stdlib.h>
+constexpr bool kProbe = true;
+inline int qt_knob(const char* name, int def) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : def;
+}
+inline const char* qt_knob_str(const char* name) { return getenv(name); }
+#else
+constexpr bool kProbe = false;
+inline int qt_knob(const char*, int def) { return def; }
+inline const char* qt_knob_str(const char*) { return nullptr; }
+#endif
 
 QT_DEV float bf2f(bf16_t h) { return __uint_as_float(((unsigned)h) << 16); }
 QT_DEV bf16_t f2bf(float f) {  // round-to-nearest-even (activations are finite)

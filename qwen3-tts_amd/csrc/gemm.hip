@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256) void igemm_k(GemmP p) {
 // 106.8 us = 320 TFLOP/s).  Same operand rounding and per-element k order as igemm_k.
 constexpr int PF_BM = 128, PF_BK = 64, PF_AST = PF_BK + 8;  // A LDS row stride (bf16): 144 B
 
-template <typename AT, typename OT, int NTB, bool P2>
+template <typename AT, typename OT, int NTB>
 __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   constexpr int CT = NTB / 2;                 // column tiles per wave
   constexpr int BT = NTB * 2;                 // B fragments (1 KiB) per stage
@@ -655,7 +655,6 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
   const AT* Ar = (const AT*)p.A + (long long)(arow ? m0 + ar : 0) * p.lda;
   float sst = 0.f;
   u32x4_t ra[AE], rb[BPT];
-  u32x4_t ra2[P2 ? AE : 1], rb2[P2 ? BPT : 1];  // second register set: two stages of loads in flight (P2)
   auto load_stage = [&](int st, u32x4_t* ra, u32x4_t* rb) {
     const int k0 = st * PF_BK + ah * 32;
 #pragma unroll
@@ -725,33 +724,14 @@ __global__ __launch_bounds__(256) void gemm_pf_k(GemmP p) {
     }
   };
   load_stage(0, ra, rb);
-  if constexpr (P2) {
-    // stage s is multiplied from LDS buffer s & 1 while stage s + 1 waits in one register set and stage s + 2 is
-    // loaded into the other: two stages of global latency hidden instead of one
-    if (S > 1) load_stage(1, ra2, rb2);
-    store_stage(0, ra, rb);
+  store_stage(0, ra, rb);
+  __syncthreads();
+  for (int st = 0; st < S; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < S) load_stage(st + 1, ra, rb);
+    compute(buf);
+    if (st + 1 < S) store_stage(buf ^ 1, ra, rb);
     __syncthreads();
-    for (int st = 0; st < S; st += 2) {
-      if (st + 2 < S) load_stage(st + 2, ra, rb);
-      compute(0);
-      if (st + 1 < S) store_stage(1, ra2, rb2);
-      __syncthreads();
-      if (st + 1 >= S) break;
-      if (st + 3 < S) load_stage(st + 3, ra2, rb2);
-      compute(1);
-      if (st + 2 < S) store_stage(0, ra, rb);
-      __syncthreads();
-    }
-  } else {
-    store_stage(0, ra, rb);
-    __syncthreads();
-    for (int st = 0; st < S; ++st) {
-      const int buf = st & 1;
-      if (st + 1 < S) load_stage(st + 1, ra, rb);
-      compute(buf);
-      if (st + 1 < S) store_stage(buf ^ 1, ra, rb);
-      __syncthreads();
-    }
   }
   if (norm) {
     const float s2 = sst + __shfl_xor(sst, 1, 64);
@@ -908,7 +888,7 @@ void launch_gemv_f(const GemmP& p, int nt, hipStream_t s) {
 // fold factor from the rows per block (bf16 weights): 4 for <= 4 rows, 2 for <= 8 (QT_GEMV_FOLD=1 disables)
 template <typename WT, typename AT, typename OT, int WPB, int U>
 void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
-  static const int fold_env = [] { const char* e = getenv("QT_GEMV_FOLD"); return e ? atoi(e) : 4; }();
+  static const int fold_env = qt_knob("QT_GEMV_FOLD", 4);
   if constexpr (sizeof(WT) == 2) {
     if (fold_env >= 4 && p.mr <= 4) return launch_gemv_f<WT, AT, OT, WPB, U, 4>(p, nt, s);
     if (fold_env >= 2 && p.mr <= 8) return launch_gemv_f<WT, AT, OT, WPB, U, 2>(p, nt, s);
@@ -921,7 +901,7 @@ void launch_gemv_u(const GemmP& p, int nt, hipStream_t s) {
 // QT_GEMV_U (4 / 8) overrides for A/B measurement.
 template <typename WT, typename AT, typename OT, int WPB>
 void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
-  static const int u_env = [] { const char* e = getenv("QT_GEMV_U"); return e ? atoi(e) : 0; }();
+  static const int u_env = qt_knob("QT_GEMV_U", 0);
   const int u = u_env ? u_env : ((per > 4 && per <= 8) ? 8 : 4);
   if (u >= 8) launch_gemv_u<WT, AT, OT, WPB, 8>(p, nt, s);
   else launch_gemv_u<WT, AT, OT, WPB, 4>(p, nt, s);
@@ -930,21 +910,19 @@ void launch_gemv(const GemmP& p, int nt, int per, hipStream_t s) {
 // largest row count run as the decode GEMV over row groups of gemv_mr() rows (QT_GEMV_MAX_M / QT_GEMV_MR override,
 // measurement; 16 = decode only)
 inline int gemv_max_m() {
-  static const int v = [] { const char* e = getenv("QT_GEMV_MAX_M"); return e ? atoi(e) : 256; }();
+  static const int v = qt_knob("QT_GEMV_MAX_M", 256);
   return v;
 }
 inline int gemv_mr() {
-  static const int v = [] { const char* e = getenv("QT_GEMV_MR"); return e ? atoi(e) : 16; }();
+  static const int v = qt_knob("QT_GEMV_MR", 16);
   return std::max(1, std::min(16, v));
 }
 
 // largest row count served by the skinny GEMM gemm_sk_k (QT_SK=0 disables it: measurement)
 inline int sk_max_m() {
   static const int v = [] {
-    const char* e = getenv("QT_SK");
-    if (e && atoi(e) == 0) return 0;
-    const char* m = getenv("QT_SK_MAX_M");  // (measurement)
-    return m ? std::min(atoi(m), 64) : 48;  // (48 vs 64: bench --workload vd64 451 vs 442 audio-s/s)
+    if (qt_knob("QT_SK", 1) == 0) return 0;
+    return std::min(qt_knob("QT_SK_MAX_M", 48), 64);  // (48 vs 64: bench --workload vd64 451 vs 442 audio-s/s)
   }();
   return v;
 }
@@ -952,29 +930,29 @@ inline int sk_max_m() {
 // largest row count of a conv routed to im2col + the linear GEMMs (QT_IM2COL_MAX_M, measurement)
 inline int im2col_max_m() {
   // (first streamed window at B = 8: 256 rows 1.70 ms, 512 1.39, 1024 1.39, 2048 1.40; profiles/r03_codec_first_window_im2col.txt)
-  static const int v = [] { const char* e = getenv("QT_IM2COL_MAX_M"); return e ? atoi(e) : 1024; }();
+  static const int v = qt_knob("QT_IM2COL_MAX_M", 1024);
   return v;
 }
 
 // smallest row count routed to the LDS-tiled implicit GEMM (QT_IGEMM_MIN_M overrides, measurement)
 inline int igemm_min_m() {
-  static const int v = [] { const char* e = getenv("QT_IGEMM_MIN_M"); return e ? atoi(e) : 128; }();
+  static const int v = qt_knob("QT_IGEMM_MIN_M", 128);
   return v;
 }
 
 // the LDS-staged prefill GEMM (gemm_pf_k) for taps == 0 linears; QT_PF=0 keeps them on igemm_k (measurement)
 inline bool pf_on() {
-  static const bool v = [] { const char* e = getenv("QT_PF"); return e ? atoi(e) != 0 : true; }();
+  static const bool v = (qt_knob("QT_PF", 1) != 0);
   return v;
 }
 // fewest rows served by gemm_pf_k (QT_PF_MIN_M, measurement; default the igemm_k threshold)
 inline int pf_min_m() {
-  static const int v = [] { const char* e = getenv("QT_PF_MIN_M"); return e ? atoi(e) : 0; }();
+  static const int v = qt_knob("QT_PF_MIN_M", 0);
   return v;
 }
 // widest output served by gemm_pf_k (QT_PF_NMAX, measurement; 0 = any)
 inline int pf_nmax() {
-  static const int v = [] { const char* e = getenv("QT_PF_NMAX"); return e ? atoi(e) : 0; }();
+  static const int v = qt_knob("QT_PF_NMAX", 0);
   return v;
 }
 
@@ -989,7 +967,7 @@ bool pf_route(const GemmP& p) {
 
 // gemm_pf2_k (deep-pipelined LDS-DMA prefill GEMM, gemm_pf2.hip): QT_PF2=0 keeps gemm_pf_k (A/B)
 inline int pf2_mode() {
-  static const int v = [] { const char* e = getenv("QT_PF2"); return e ? atoi(e) : 1; }();
+  static const int v = qt_knob("QT_PF2", 1);
   return v;
 }
 
@@ -1027,11 +1005,8 @@ int launch(const GemmP& p, hipStream_t s) {
     // prefill linears: LDS-staged A and B, 128 x 128 tiles (128 x 64 when that leaves < 256 blocks)
     const int mt = (p.M + PF_BM - 1) / PF_BM;
     const bool narrow = (long long)mt * ((nt + 7) / 8) < 256;
-    static const bool p2 = [] { const char* e = getenv("QT_PF_P2"); return e ? atoi(e) != 0 : false; }();
-    if (narrow && p2) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4, true>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
-    else if (narrow) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4, false>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
-    else if (p2) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8, true>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8, false>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
+    if (narrow) hipLaunchKernelGGL((gemm_pf_k<AT, OT, 4>), dim3(mt, (nt + 3) / 4), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_pf_k<AT, OT, 8>), dim3(mt, (nt + 7) / 8), dim3(256), 0, s, p);
   } else if (sizeof(WT) == 2 && p.a_index == nullptr && p.gamma == nullptr && p.N >= 32 &&
              p.M >= (p.taps > 0 ? 16 : igemm_min_m()) &&
              (p.taps == 0 ? p.Klog % 8 == 0 : IG_BM + (p.taps - 1) * p.dil <= 256 * IG_GPT / 4) && !p.no_igemm) {
@@ -1039,9 +1014,9 @@ int launch(const GemmP& p, hipStream_t s) {
     const int t_out = p.taps == 0 ? p.M : p.t_out, batches = p.taps == 0 ? 1 : p.M / p.t_out;
     // column tile per block: 6 x 16 for 96 / 192-channel layers (no idle tiles, the snake-staged window is
     // shared by all of a row tile's columns), else 8 x 16; QT_IGEMM_CFG = "NT,MI" overrides (measurement)
-    static const int cfg = [] { const char* e = getenv("QT_IGEMM_CFG"); return e ? atoi(e) * 10 + atoi(e + 2) : 0; }();
+    static const int cfg = [] { const char* e = qt_knob_str("QT_IGEMM_CFG"); return e ? atoi(e) * 10 + atoi(e + 2) : 0; }();
     // QT_IGEMM_G2 = 0 selects the 4 x 1 wave layout (measurement); default 2 x 2
-    static const int g2 = [] { const char* e = getenv("QT_IGEMM_G2"); return e ? atoi(e) : 1; }();
+    static const int g2 = qt_knob("QT_IGEMM_G2", 1);
     int ntb = (nt % 6 == 0 && nt <= 12) ? 6 : 8, mi = 2;
     // short windows (a streamed codec window, 1-3 frames x batch rows per conv): 64-row tiles and 4 (6) column
     // tiles per block when the default tiling leaves fewer than 256 blocks -- the first streamed window's feed
@@ -1129,7 +1104,7 @@ __global__ __launch_bounds__(256) void im2col_k(GemmP p, bf16_t* __restrict__ ou
 // The im2col image lives in the upper half of the caller's workspace.  QT_IM2COL=0 disables (measurement).
 constexpr long long IM2COL_WS = 16ll << 20, IM2COL_OFF = 8ll << 20;
 inline bool im2col_route(const qt_gemm_args* a) {
-  static const int env = [] { const char* e = getenv("QT_IM2COL"); return e ? atoi(e) : 1; }();
+  static const int env = qt_knob("QT_IM2COL", 1);
   if (!env || a->taps <= 0 || a->w_dtype != QT_BF16 || a->M <= 0 || a->M > im2col_max_m() || a->rmsnorm ||
       a->gamma != nullptr || a->a_index != nullptr || !a->ws || a->ws_bytes < IM2COL_WS || a->t_out <= 0 ||
       a->cin_pad % 32 || a->cin % 8 || a->splitk == 1)
@@ -1184,11 +1159,11 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   if (a->a_act != QT_AACT_NONE && a->a_act != QT_AACT_ELU) return QT_ERR_ARG;
   if (a->act < QT_ACT_NONE || a->act > QT_ACT_RELU_TANH) return QT_ERR_ARG;
   p.a_elu = a->a_act == QT_AACT_ELU;
-  static const int no_ig = [] { const char* e = getenv("QT_NO_IGEMM"); return e ? atoi(e) : 0; }();
+  static const int no_ig = qt_knob("QT_NO_IGEMM", 0);
   p.no_igemm = no_ig;
   // weights streamed once per frame (talker-size matrices) bypass cache retention so the re-read code-predictor
   // weights stay in L2 / Infinity Cache; QT_GEMV_NT=0/1 forces it off/on for every decode GEMV (measurement)
-  static const int nt_env = [] { const char* e = getenv("QT_GEMV_NT"); return e ? atoi(e) : -1; }();
+  static const int nt_env = qt_knob("QT_GEMV_NT", -1);
   const long long wbytes = (long long)((a->N + 15) / 16) * 16 * p.Kp * (a->w_dtype == QT_BF16 ? 2 : 4);
   p.ntl = nt_env >= 0 ? nt_env : (wbytes >= (16ll << 20));
   // split-K for the decode GEMV when it has too few column tiles to fill 256 CUs twice
@@ -1201,7 +1176,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   }
   // wide grids use smaller blocks so several fit per CU (fewer block rounds; measured: N=12288 K=2048
   // 14.7 us at 16 waves/block -> 12.0 at 4); QT_GEMV_WPB overrides the cap for A/B measurement
-  static const int wpb_env = [] { const char* e = getenv("QT_GEMV_WPB"); return e ? atoi(e) : 0; }();
+  static const int wpb_env = qt_knob("QT_GEMV_WPB", 0);
   const int ntc = (a->N + 15) / 16;
   p.wpb_max = wpb_env > 0 ? wpb_env : (ntc > 512 ? 4 : (ntc > 256 ? 8 : 16));
   const int ntl = (a->N + 15) / 16, ktl = p.Kp / KT;
@@ -1212,7 +1187,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
     // 2048x6144 11.4 (no split) / 10.9 (2) / 10.3 us (4), 1024x3072 8.5 / 7.6 / 7.1 us; other shapes lose.
     // In the frame graph split 2 wins (bench 158.6 vs 157.2 audio-s/s, same box): QT_GEMV_SPLIT_AUTO overrides
     const int wpb1 = ktl >= 48 ? 16 : (ktl >= 16 ? 8 : 4), per1 = (ktl + wpb1 - 1) / wpb1;
-    static const int ks_auto = [] { const char* e = getenv("QT_GEMV_SPLIT_AUTO"); return e ? atoi(e) : 2; }();
+    static const int ks_auto = qt_knob("QT_GEMV_SPLIT_AUTO", 2);
     int ks = a->splitk > 1 ? a->splitk : ((per1 > 4 && ntl < 256) ? ks_auto : 1);
     ks = std::max(1, std::min({ks, 16, ktl / 2}));
     const size_t need = 4096 * sizeof(unsigned) + (size_t)ntl * ks * (64 * 4 + 16) * sizeof(float);
@@ -1242,7 +1217,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
   // QT_SKINNY=0 restores the round-2 rule (row-group GEMV up to 96 rows / 256 rows of <= 2048 columns).
   p.sk = 0;
   p.pf_small = 0;
-  static const int skinny_env = [] { const char* e = getenv("QT_SKINNY"); return e ? atoi(e) : 1; }();
+  static const int skinny_env = qt_knob("QT_SKINNY", 1);
   const bool skinny = skinny_env != 0 && a->M > 16 && a->M <= 256 && a->taps == 0 && a->w_dtype == QT_BF16 &&
                       a->a_dtype == QT_BF16 && a->K % 64 == 0 && a->a_index == nullptr && a->gamma == nullptr &&
                       a->a_act == QT_AACT_NONE && a->snake_alpha == nullptr && a->lda % 8 == 0 &&
@@ -1258,7 +1233,7 @@ extern "C" int qt_gemm(const qt_gemm_args* a, void* stream) {
       p.pf_small = 1;
     }
   }
-  static const int rg_env = [] { const char* e = getenv("QT_GEMV_RG"); return e ? atoi(e) : 0; }();
+  static const int rg_env = qt_knob("QT_GEMV_RG", 0);
   if (a->M <= 16 && a->taps == 0 && a->w_dtype == QT_BF16 && a->K % KT == 0 && a->gamma == nullptr) {
     // four groups of 2 rows for <= 64 tiles (CP down 6.5 -> 5.8 us; 128-tile shapes lose with four)
     const int rg = rg_env > 0 ? rg_env : (a->M > 4 ? (ntl <= 64 ? 4 : (ntl <= 128 ? 2 : 1)) : 1);

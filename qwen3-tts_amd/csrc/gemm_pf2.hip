@@ -398,7 +398,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
 // (>= 16 stages of 64 per split; wide outputs measured slower split: 1.7B q/k/v at 80 rows 15.5 -> 17.9 us) when the caller's workspace holds the split records (QT_PF2_SPLIT=0 disables, measurement)
 template <int BM, int NTB, int WM, int WN>
 int pf2_splits(const GemmP& p, int nwg) {
-  static const int env = [] { const char* e = getenv("QT_PF2_SPLIT"); return e ? atoi(e) : 1; }();
+  static const int env = qt_knob("QT_PF2_SPLIT", 1);
   const int S = p.Klog / 64;
   if (!env || p.part == nullptr || p.cnt == nullptr || p.N > 2048 || nwg >= 192 || S < 32) return 1;
   int ks = std::min({PF2_KS_MAX, 256 / nwg, S / 16});
@@ -460,7 +460,7 @@ constexpr Pf2Cfg PF2_CFGS[] = {
     {9, 256, 160, 1, 95000.f, 95000.f, 10000.f}, // 4 waves, wave tile 128 x 80
 };
 inline int pf2_cfg_env() {
-  static const int v = [] { const char* e = getenv("QT_PF2_CFG"); return e ? atoi(e) : 0; }();
+  static const int v = qt_knob("QT_PF2_CFG", 0);
   return v;
 }
 inline int pf2_pick(int M, int N, int K) {

@@ -151,7 +151,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
       x = -INFINITY;
     s[j] = x;
   }
-  if (pk.stop == 1) {
+  if (kProbe && pk.stop == 1) {
     if (s[0] + s[PER - 1] == 1234.5f) p.tok_out[r] = 0;
     return;
   }
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
         base += __popcll(m);
       }
       if (lane == 0) nc_s[w] = base;
-      if (pk.stop == 6) {
+      if (kProbe && pk.stop == 6) {
         if (lane == 0 && base == 12345) p.tok_out[r] = 0;
         return;
       }
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
           g = okey_inv(mk) - __logf(-__logf(u));
         }
         __syncthreads();
-        if (pk.stop == 7) {
+        if (kProbe && pk.stop == 7) {
           if (g == 1.5f && tk_s == 12345u) p.tok_out[r] = 0;
           return;
         }
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     }
     unsigned tk = 0;  // keep keys >= tk
     if (!fast) mx = block_max(mx, sh);
-    if (pk.stop == 2) {
+    if (kProbe && pk.stop == 2) {
       if (mx == 1234.5f) p.tok_out[r] = 0;
       return;
     }
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
         tk = shtk;
       }
     }
-    if (pk.stop == 3) {
+    if (kProbe && pk.stop == 3) {
       if (tk == 12345u) p.tok_out[r] = 0;
       return;
     }
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     const float total = ((sh[0] + sh[1]) + sh[2]) + sh[3];
     const float inc = scan + off;
     const float excl = lane == 0 ? off : prev + off;
-    if (pk.stop == 4) {
+    if (kProbe && pk.stop == 4) {
       if (inc == 1234.5f) p.tok_out[r] = 0;
       return;
     }
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(NT) void sample_k(SK pk) {
     if (tid == 0) p.pick[off] = tok;
     tok = p.force[off];
   }
-  if (pk.stop == 5) {
+  if (kProbe && pk.stop == 5) {
     if (tid == 0) p.tok_out[r] = tok;
     return;
   }
@@ -604,7 +604,7 @@ extern "C" int qt_sample(const qt_sample_args* a, void* stream) {
   if (a->emb2_table && (!a->emb_table || !a->emb2_out || a->emb2_dim % 4 || a->emb2_ld % 4)) return QT_ERR_SHAPE;
   if (a->force && (!a->pick || !a->codes)) return QT_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  static const int stop = [] { const char* e = getenv("QT_SAMPLE_STOP"); return e ? atoi(e) : 0; }();
+  static const int stop = qt_knob("QT_SAMPLE_STOP", 0);
   const SK k{*a, stop};
   if (a->V <= NT * 8) hipLaunchKernelGGL(sample_k<8>, dim3(a->R), dim3(NT), 0, st, k);
   else if (a->V <= NT * 12) hipLaunchKernelGGL(sample_k<12>, dim3(a->R), dim3(NT), 0, st, k);

@@ -87,7 +87,7 @@ class SampleArgs(ctypes.Structure):
 
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
-           "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes",
+           "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -145,6 +145,7 @@ def load_library(path: str = LIB_PATH):
         "qt_decode_attn_ws_bytes": [c_int, c_int, c_int, c_int, c_int],
         "qt_decode_attn_oproj": [P, P],
         "qt_attn_oproj_ws_bytes": [c_int, c_int],
+        "qt_attn_oproj_resident_blocks": [],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],
@@ -180,6 +181,16 @@ def env_int(name: str, default: int) -> int:
     import re
     m = re.match(r"\s*([+-]?\d+)", v)
     return int(m.group(1)) if m else 0
+
+
+# the probe library (build.py --probe) reads the measurement knobs; the product library ignores the environment, and
+# so do the host-side mirrors of its knobs (lib_knob)
+PROBE = os.path.basename(LIB_PATH).endswith("_probe.so")
+
+
+def lib_knob(name: str, default: int) -> int:
+    """A knob the library reads too (e.g. QT_PF): honoured only with the probe library, like the library's own."""
+    return env_int(name, default) if PROBE else default
 
 
 def check(rc: int, what: str):

@@ -393,6 +393,8 @@ class TTSModel:
             # codes of frames [0, frames) are final; column `frames` holds the next cb0 (EOS of finishing rows)
             codes = torch.cat([s.codes[:, :frames + 1] for s in sessions], 0)  # int32 [B, frames+1, 16], device
             c0 = codes[:, :, 0].cpu()
+            if not final and sessions[0].watch is not None:  # (synchronised above) before any audio is handed out
+                sessions[0].watch.check()
             for b in range(B):
                 if end[b] is None:
                     hit = (c0[b, emitted:] == eos).nonzero()
@@ -543,6 +545,10 @@ class TTSModel:
                         if end[b] is not None and cap[b] is None:
                             cap[b] = up * (pre_nz[b] + int((c0[b, :end[b]] != 0).sum()))
                     scanned = frames
+                    # the host just synchronised on these frames: a hand-off give-up among them raises before any
+                    # of their audio is handed out
+                    if sessions[0].watch is not None:
+                        sessions[0].watch.check()
                 # decode positions (prefix + generated) available for every row; the sequence length once all ended
                 t_end = max(R[b] + end[b] for b in range(B)) if all(x is not None for x in end) else None
                 avail = t_end if t_end is not None else min(R[b] + frames for b in range(B) if end[b] is None)

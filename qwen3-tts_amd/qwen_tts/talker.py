@@ -141,7 +141,7 @@ QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
 PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
 # large-M prefill linears on gemm_pf_k (LDS-staged bf16 A and B): the prefill keeps the bf16 residual shadow at any
 # row count, so its RMS GEMMs read bf16 A too; QT_PF=0 (read by the library as well) keeps igemm_k (A/B)
-PF = _hip.env_int("QT_PF", 1) != 0  # parsed as the library parses it (C atoi)
+PF = _hip.lib_knob("QT_PF", 1) != 0  # as the library reads it (probe builds only)
 # static prefill buffers (+ captured graphs) kept per session: the most recently used prompt lengths, LRU-evicted
 PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
 # the generation config's min_new_tokens (M:2044-2066): EOS is suppressed while a row has generated fewer tokens
@@ -190,14 +190,59 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     return sc
 
 
+HANDOFF_ERROR = ("qt_decode_attn_oproj: a head-split hand-off timed out (blocks not co-resident?); outputs of this "
+                 "request are invalid (QT_AO_HS=0 selects the form without hand-offs)")
+
+
+def _flag_word(s):
+    ws = s.cp.sc.get("ao_ws")
+    return None if ws is None else ws[:4].view(torch.int32)
+
+
 def check_handoffs(sessions):
     """Raise if a head-split attention + o_proj launch of these sessions gave up waiting for a hand-off (the sticky
-    flag in its workspace): its output rows would hold stale partial sums.  Reads a device word (host sync)."""
+    flag in its workspace): its output rows would hold stale partial sums.  The flag is cleared first, so a pooled
+    session serves its next request normally.  Reads a device word (host sync)."""
+    bad = False
     for s in sessions:
-        ws = s.cp.sc.get("ao_ws")
-        if ws is not None and int(ws[:4].view(torch.int32).item()) != 0:
-            raise RuntimeError("qt_decode_attn_oproj: a head-split hand-off timed out (blocks not co-resident?); "
-                               "outputs of this session are invalid (QT_AO_HS=0 selects the form without hand-offs)")
+        f = _flag_word(s)
+        if f is not None and int(f.item()) != 0:
+            f.zero_()
+            bad = True
+    if bad:
+        raise RuntimeError(HANDOFF_ERROR)
+
+
+class HandoffWatch:
+    """The sessions' hand-off flags copied to pinned host memory behind an event, without a host sync: armed after
+    frames are queued, read once the event has completed (e.g. after the caller synchronised on a chunk's output).
+    check() raises (and clears the device flag) when a flag was set."""
+
+    def __init__(self, sessions):
+        self.items = []
+        for s in sessions:
+            f = _flag_word(s)
+            if f is None:
+                continue
+            h = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            h.copy_(f, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.items.append((s, h, ev))
+
+    def check(self, block: bool = True) -> bool:
+        """True once every copy has landed and no flag was set; False when not landed yet (block=False)."""
+        bad = False
+        for s, h, ev in self.items:
+            if not block and not ev.query():
+                return False
+            ev.synchronize()
+            if int(h[0]) != 0:
+                _flag_word(s).zero_()
+                bad = True
+        if bad:
+            raise RuntimeError(HANDOFF_ERROR)
+        return True
 
 
 def _attn_oproj_ok(st: _Stack) -> bool:
@@ -326,6 +371,7 @@ class Session:
         self.prefill = OrderedDict()
         self.slot_prefill = OrderedDict()  # P -> static single-request prefill buffers (serve() refills); LRU
         self.busy = False  # held by a live decode_iter (a suspended stream() generator included)
+        self.watch = None  # HandoffWatch armed at the last yield of decode_iter
         self.cp = CPLane(self, eng, 0, B, self.ws)
 
 
@@ -612,6 +658,7 @@ class TalkerEngine:
         # EOS polling without a host sync: every `check_every` frames the all-finished flag is copied to pinned
         # memory behind an event; the copy from the previous window is read once its event has completed
         pending = []
+        watch = None  # hand-off flags as of the previous yield (checked before the next chunk is handed out)
         while frames < max_frames:
             early = early_first and frames == 0 and next_yield == 1 and max_frames > 1
             for s, st in zip(sessions, streams):
@@ -623,6 +670,12 @@ class TalkerEngine:
             if next_yield and frames == next_yield and frames < max_frames:
                 for st in streams:
                     main.wait_stream(st)
+                if watch is not None:  # the caller consumed the previous chunk: those frames are done
+                    watch.check()
+                with torch.cuda.stream(main):
+                    watch = HandoffWatch(sessions)
+                for s in sessions:  # a caller that synchronised on these frames checks it before using them
+                    s.watch = watch
                 yield sessions, frames, False
                 interval = min(every, 2 * interval) if grow else every
                 next_yield = frames + interval if every else 0
@@ -754,9 +807,13 @@ class TalkerEngine:
                         hc.copy_(s.codes[b], non_blocking=True)
                         hh.copy_(s.hiddens[b], non_blocking=True)
                         hs.copy_(s.step[b:b + 1], non_blocking=True)
+                        hf = None
+                        if _flag_word(s) is not None:  # the hand-off flag as of this request's last frame
+                            hf = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                            hf.copy_(_flag_word(s), non_blocking=True)
                         ev = torch.cuda.Event()
                         ev.record()
-                        harvests.append((slot_req[b], hc, hh, hs, ev))
+                        harvests.append((slot_req[b], hc, hh, hs, hf, ev))
                         epoch[b] += 1
                         start[b] = frame
                         slot_req[b] = queue.pop(0) if queue else -1
@@ -766,7 +823,9 @@ class TalkerEngine:
                         else:
                             s.finished[b:b + 1].fill_(1)  # idle slot: emits EOS until the session ends
                     while harvests and harvests[0][-1].query():
-                        i, hc, hh, hs, _ = harvests.pop(0)
+                        i, hc, hh, hs, hf, _ = harvests.pop(0)
+                        if hf is not None and int(hf[0]) != 0:  # never hand out a request decoded on stale partials
+                            check_handoffs([s])
                         # frames [0, F) are final: F = the first EOS in cb0 (within the row's frame range), else the
                         # row's frame count (max_new_tokens - 1)
                         F = min(int(hs[0]), cap_i[i])
