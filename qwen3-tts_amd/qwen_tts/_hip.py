@@ -70,6 +70,18 @@ class AttnOprojArgs(ctypes.Structure):
                 ("ws_bytes", c_ll)]
 
 
+P8 = c_void_p * 8
+
+
+class CpStepArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("n_layers", c_int), ("Lmax", c_int), ("const_pos", c_int), ("V", c_int),
+                ("eps", c_float), ("cos_tab", c_void_p), ("sin_tab", c_void_p),
+                ("w_qkv", P8), ("w_o", P8), ("w_gu", P8), ("w_down", P8), ("q_norm", P8), ("k_norm", P8),
+                ("k_cache", P8), ("v_cache", P8), ("w_lm", c_void_p), ("x", c_void_p), ("ldx", c_ll),
+                ("qkv0", c_void_p), ("ldq", c_ll), ("logits", c_void_p), ("ldl", c_ll), ("ws", c_void_p),
+                ("ws_bytes", c_ll)]
+
+
 class SampleArgs(ctypes.Structure):
     _fields_ = [("logits", c_void_p), ("R", c_int), ("V", c_int), ("ld", c_ll), ("seen", c_void_p),
                 ("rep_penalty", c_float), ("n_generated", c_void_p), ("min_new_tokens", c_int), ("eos_id", c_int),
@@ -88,6 +100,7 @@ class SampleArgs(ctypes.Structure):
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
+           "qt_cp_step", "qt_cp_step_ws_bytes", "qt_cp_step_supported",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -146,6 +159,8 @@ def load_library(path: str = LIB_PATH):
         "qt_decode_attn_oproj": [P, P],
         "qt_attn_oproj_ws_bytes": [c_int, c_int],
         "qt_attn_oproj_resident_blocks": [],
+        "qt_cp_step": [P, P], "qt_cp_step_ws_bytes": [],
+        "qt_cp_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],

@@ -278,6 +278,34 @@ def decode_attn_oproj(qkv, R, Hq, Hkv, D, q_norm, k_norm, eps, cos, sin, kc, vc,
     check(_hip.lib().qt_decode_attn_oproj(ctypes.byref(a), stream()), "qt_decode_attn_oproj")
 
 
+def cp_step_ws_bytes():
+    return int(_hip.lib().qt_cp_step_ws_bytes())
+
+
+def cp_step_supported(H, I, Hq, Hkv, D, n_layers, V) -> bool:
+    return bool(_hip.lib().qt_cp_step_supported(H, I, Hq, Hkv, D, n_layers, V))
+
+
+def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, sin, eps, logits, ws):
+    """qt_cp_step: one code-predictor decode step (every layer + final norm + lm_head) in one persistent launch.
+    layers: the code predictor's _Layer objects (tiled qkv / o / gate-up / down, q_norm / k_norm); kcs / vcs: per-layer
+    bf16 caches [R][Hkv][Lmax][D]; x fp32 [R][H] input rows; qkv0 fp32 [R][qkv] layer-0 q/k/v rows; logits fp32 [R][V].
+    ws: zeroed uint8 scratch of cp_step_ws_bytes() kept across launches (word 0: the sticky hand-off error flag)."""
+    a = _hip.CpStepArgs()
+    a.R, a.n_layers, a.Lmax, a.const_pos, a.V, a.eps = R, len(layers), Lmax, const_pos, w_lm.N, eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    for i, L in enumerate(layers):
+        a.w_qkv[i], a.w_o[i], a.w_gu[i], a.w_down[i] = ptr(L.qkv.w), ptr(L.o.w), ptr(L.gu.w), ptr(L.down.w)
+        a.q_norm[i], a.k_norm[i] = ptr(L.q_norm), ptr(L.k_norm)
+        a.k_cache[i], a.v_cache[i] = ptr(kcs[i]), ptr(vcs[i])
+    a.w_lm = ptr(w_lm.w)
+    a.x, a.ldx = ptr(x), x.stride(0)
+    a.qkv0, a.ldq = ptr(qkv0), qkv0.stride(0)
+    a.logits, a.ldl = ptr(logits), logits.stride(0)
+    a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    check(_hip.lib().qt_cp_step(ctypes.byref(a), stream()), "qt_cp_step")
+
+
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,

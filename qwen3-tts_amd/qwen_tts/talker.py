@@ -132,6 +132,10 @@ ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
 # less L2 -> CU traffic than the (column group, row) form (profiles/r04_pmc_attn_oproj*.json), 7.71 -> 7.03 us per
 # launch, bench 200.2 -> 202.8 audio-s/s (profiles/r04_bench_ab_ao_hs.txt).  QT_AO_HS=0 keeps the other form (A/B)
 AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
+# code-predictor decode steps as ONE persistent launch each (qt_cp_step: every layer + lm_head, in-launch hand-offs)
+# instead of ~21 dependent launches (bf16 mode with the layer-0 q/k/v tables, <= 8 rows); QT_CP_ENGINE=0 keeps the
+# launch chain (A/B)
+CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -190,24 +194,45 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     return sc
 
 
-HANDOFF_ERROR = ("qt_decode_attn_oproj: a head-split hand-off timed out (blocks not co-resident?); outputs of this "
-                 "request are invalid (QT_AO_HS=0 selects the form without hand-offs)")
+HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step; blocks not "
+                 "co-resident?); outputs of this request are invalid (QT_AO_HS=0 / QT_CP_ENGINE=0 select the forms "
+                 "without hand-offs)")
+
+
+def _flag_words(s):
+    """The sticky hand-off error words of a session's in-launch hand-off kernels (head-split attention + o_proj,
+    the code-predictor step engine), int32 device views."""
+    out = []
+    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws):
+        if ws is not None:
+            out.append(ws[:4].view(torch.int32))
+    return out
 
 
 def _flag_word(s):
-    ws = s.cp.sc.get("ao_ws")
-    return None if ws is None else ws[:4].view(torch.int32)
+    """All of the session's error words as one device int32 (their OR), or None when it runs no hand-off kernel."""
+    fs = _flag_words(s)
+    if not fs:
+        return None
+    if len(fs) == 1:
+        return fs[0]
+    return torch.stack(fs).amax(0)
+
+
+def _clear_flags(s):
+    for f in _flag_words(s):
+        f.zero_()
 
 
 def check_handoffs(sessions):
-    """Raise if a head-split attention + o_proj launch of these sessions gave up waiting for a hand-off (the sticky
-    flag in its workspace): its output rows would hold stale partial sums.  The flag is cleared first, so a pooled
-    session serves its next request normally.  Reads a device word (host sync)."""
+    """Raise if an in-launch hand-off of these sessions gave up waiting (the sticky flag in a workspace): its output
+    rows would hold stale partial sums.  The flags are cleared first, so a pooled session serves its next request
+    normally.  Reads device words (host sync)."""
     bad = False
     for s in sessions:
         f = _flag_word(s)
         if f is not None and int(f.item()) != 0:
-            f.zero_()
+            _clear_flags(s)
             bad = True
     if bad:
         raise RuntimeError(HANDOFF_ERROR)
@@ -238,7 +263,7 @@ class HandoffWatch:
                 return False
             ev.synchronize()
             if int(h[0]) != 0:
-                _flag_word(s).zero_()
+                _clear_flags(s)
                 bad = True
         if bad:
             raise RuntimeError(HANDOFF_ERROR)
@@ -268,6 +293,9 @@ class CPLane:
         self.kv = ([k[b0:b1] for k in s.cp_kv[0]], [v[b0:b1] for v in s.cp_kv[1]])
         self.sc = _scratch(2 * nb, c, dev, attn_oproj=nb <= ATTN_OPROJ_MAX)
         self.ws = ws
+        # the step engine's hand-off granules + launch counter (zeroed once, kept across launches)
+        self.ce_ws = (torch.zeros(K.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+                      if eng.cp_engine and nb <= 8 else None)
         self.logits = torch.zeros(nb, eng.Vc, dtype=torch.float32, device=dev)
         self.tok = s.cp_tok[b0:b1]
         self.codes = s.codes[b0:b1]
@@ -420,6 +448,11 @@ class TalkerEngine:
                 out = torch.empty(tab.shape[0], c.qkv_w, dtype=torch.float32, device=dev)
                 K.gemm(t16, L0.qkv, out, tab.shape[0], Hc, c.qkv_w, rms=True, eps=c.eps)
                 self.cp_qkv_tabs.append(out)
+        # the code-predictor step engine (qt_cp_step): bf16, layer-0 q/k/v tables, the shapes it is built for, and a
+        # device that keeps its 256 workgroups resident
+        c = self.cp
+        self.cp_engine = (CP_ENGINE and self.cp_qkv_tabs is not None and
+                          K.cp_step_supported(c.H, c.I, c.Hq, c.Hkv, c.D, c.n_layers, self.Vc))
         self._sessions: Dict[tuple, List[Session]] = {}
         torch.cuda.synchronize()
 
@@ -562,13 +595,22 @@ class TalkerEngine:
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
             x16 = None if ln.x16 is None else ln.x16[:nb]
+            if ln.ce_ws is not None:  # the whole step (5 layers + lm_head[g]) in one persistent launch
+                K.cp_step(c.layers, self.lm_heads[g], x, ln.sc["qkv"][:nb], nb, ln.kv[0], ln.kv[1], s.cp_L, g + 1,
+                          c.cos, c.sin, c.eps, ln.logits, ln.ce_ws)
+                self._cp_sample(s, ln, g)
+                continue
             c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16,
                       qkv0=self.cp_qkv_tabs is not None)
             self._cp_head(s, ln, x, Hc, g, x16)
 
     def _cp_head(self, s: Session, ln: CPLane, h, ldh, g, h16=None):
-        c, gp = self.cp, s.gp
+        c = self.cp
         K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
+        self._cp_sample(s, ln, g)
+
+    def _cp_sample(self, s: Session, ln: CPLane, g):
+        c, gp = self.cp, s.gp
         K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed_ptr=s.seed, step=s.step[ln.b0:ln.b1], substep=1 + g, codes=ln.codes,
@@ -807,10 +849,10 @@ class TalkerEngine:
                         hc.copy_(s.codes[b], non_blocking=True)
                         hh.copy_(s.hiddens[b], non_blocking=True)
                         hs.copy_(s.step[b:b + 1], non_blocking=True)
-                        hf = None
-                        if _flag_word(s) is not None:  # the hand-off flag as of this request's last frame
+                        hf, fw = None, _flag_word(s)
+                        if fw is not None:  # the hand-off flags as of this request's last frame
                             hf = torch.empty(1, dtype=torch.int32, pin_memory=True)
-                            hf.copy_(_flag_word(s), non_blocking=True)
+                            hf.copy_(fw, non_blocking=True)
                         ev = torch.cuda.Event()
                         ev.record()
                         harvests.append((slot_req[b], hc, hh, hs, hf, ev))

@@ -1,0 +1,136 @@
+"""qt_cp_step (one persistent launch per code-predictor decode step: 5 layers + final norm + lm_head) against the
+launch chain it replaces (qt_gemm q/k/v, the head-split qt_decode_attn_oproj, gate/up + SwiGLU, down, lm_head GEMV) on
+the same inputs, at the code predictor's real dims (hidden 1024, 16 / 8 heads x 128, intermediate 3072, 5 layers,
+2048 codes), bf16.  Both compute in bf16 MFMA with fp32 accumulation in different summation orders, so logits and the
+appended K/V are compared within bf16 tolerance; the engine itself is deterministic (repeat launches give the same
+bits), advances its launch counter across launches on one workspace (changing row counts and cache positions) and
+never sets its hand-off error flag."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _cp_stack(dev, seed=0):
+    from oracle import load_preset
+    from qwen_tts.talker import _Stack
+    cfg, _ = load_preset("1.7b-customvoice")
+    lc = cfg["talker_config"]["code_predictor_config"]
+    g = torch.Generator().manual_seed(seed)
+    H, I, D = lc["hidden_size"], lc["intermediate_size"], lc["head_dim"]
+    nq, nkv = lc["num_attention_heads"], lc["num_key_value_heads"]
+    W = {}
+    r = lambda *s: (0.03 * torch.randn(*s, generator=g))  # noqa: E731
+    n = lambda *s: (1 + 0.1 * torch.randn(*s, generator=g))  # noqa: E731
+    for i in range(lc["num_hidden_layers"]):
+        p = f"cp.layers.{i}"
+        W[f"{p}.self_attn.q_proj.weight"] = r(nq * D, H)
+        W[f"{p}.self_attn.k_proj.weight"] = r(nkv * D, H)
+        W[f"{p}.self_attn.v_proj.weight"] = r(nkv * D, H)
+        W[f"{p}.self_attn.o_proj.weight"] = r(H, nq * D)
+        W[f"{p}.mlp.gate_proj.weight"] = r(I, H)
+        W[f"{p}.mlp.up_proj.weight"] = r(I, H)
+        W[f"{p}.mlp.down_proj.weight"] = r(H, I)
+        W[f"{p}.input_layernorm.weight"] = n(H)
+        W[f"{p}.post_attention_layernorm.weight"] = n(H)
+        W[f"{p}.self_attn.q_norm.weight"] = n(D)
+        W[f"{p}.self_attn.k_norm.weight"] = n(D)
+    W["cp.norm.weight"] = n(H)
+    st = _Stack(W, "cp", lc, torch.bfloat16, dev, 32)
+    from qwen_tts import kernels as Kn
+    lm = Kn.tile_linear((0.03 * torch.randn(lc["vocab_size"], H, generator=g)).to(dev), torch.bfloat16, gamma=st.norm)
+    return st, lm, g
+
+
+def _inputs(st, R, Lmax, g, dev):
+    from qwen_tts import kernels as Kn
+    x = torch.randn(R, st.H, generator=g).to(dev)
+    x16 = x.to(torch.bfloat16)
+    qkv0 = torch.empty(R, st.qkv_w, device=dev)
+    Kn.gemm(x16, st.layers[0].qkv, qkv0, R, st.H, st.qkv_w, rms=True, eps=st.eps)
+    kc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    vc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    return x, x16, qkv0, kc, vc
+
+
+def _chain(st, lm, x, x16, qkv0, kc, vc, R, Lmax, pos, dev):
+    """The launch chain of TalkerEngine._cp_lane for one decode step (qkv0 = layer 0's q/k/v rows)."""
+    from qwen_tts import kernels as Kn
+    from qwen_tts.talker import _scratch
+    sc = _scratch(R, st, dev, attn_oproj=True)
+    sc["qkv"][:R] = qkv0
+    meta = {"const_pos": pos}
+    st.forward(x, R, meta, (kc, vc), sc, Lmax, Lmax, decode=True, x16=x16, qkv0=True)
+    logits = torch.empty(R, lm.N, device=dev)
+    Kn.gemm(x16, lm, logits, R, st.H, lm.N, rms=True, eps=st.eps)
+    return logits
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm())
+
+
+@pytest.mark.parametrize("R,pos", [(8, 2), (8, 15), (5, 9), (1, 4)])
+def test_cp_step_matches_launch_chain(R, pos):
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    st, lm, g = _cp_stack(dev)
+    if not Kn.cp_step_supported(st.H, st.I, st.Hq, st.Hkv, st.D, st.n_layers, lm.N):
+        pytest.skip("qt_cp_step not supported on this device")
+    Lmax = 18
+    x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+    kc1, vc1 = [k.clone() for k in kc], [v.clone() for v in vc]
+    ref = _chain(st, lm, x.clone(), x16.clone(), qkv0, kc1, vc1, R, Lmax, pos, dev)
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+    outs = []
+    for _ in range(3):
+        kc2, vc2 = [k.clone() for k in kc], [v.clone() for v in vc]
+        logits = torch.full((R, lm.N), float("nan"), device=dev)
+        Kn.cp_step(st.layers, lm, x, qkv0, R, kc2, vc2, Lmax, pos, st.cos, st.sin, st.eps, logits, ws)
+        torch.cuda.synchronize()
+        outs.append((logits, kc2, vc2))
+    assert int(ws[:4].view(torch.int32).item()) == 0, "hand-off poll gave up"
+    for o in outs[1:]:  # deterministic over launches (the tags advance)
+        assert torch.equal(o[0], outs[0][0])
+    logits, kc2, vc2 = outs[0]
+    e = _rel(logits, ref)
+    print(f"\n  R={R} pos={pos}: logits rel-L2 {e:.2e}, max|d| {float((logits - ref).abs().max()):.3g} "
+          f"(|ref| max {float(ref.abs().max()):.3g}); argmax agree {(logits.argmax(-1) == ref.argmax(-1)).float().mean():.2f}")
+    assert torch.isfinite(logits).all()
+    assert e < 2e-2
+    for li in range(st.n_layers):
+        # layer 0's new key / value come from the same q/k/v rows: identical; later layers within bf16 rounding
+        if li == 0:
+            assert torch.equal(kc2[li], kc1[li]) and torch.equal(vc2[li], vc1[li])
+        else:
+            assert _rel(kc2[li][:, :, pos], kc1[li][:, :, pos]) < 2e-2
+            assert _rel(vc2[li][:, :, pos], vc1[li][:, :, pos]) < 2e-2
+            assert torch.equal(kc2[li][:, :, :pos], kc1[li][:, :, :pos])  # nothing else written
+
+
+def test_cp_step_launch_sequence_on_one_workspace():
+    """14 consecutive decode steps (positions 2..15) and changing row counts on ONE workspace, each launch against the
+    launch chain on the same inputs."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    st, lm, g = _cp_stack(dev, seed=3)
+    if not Kn.cp_step_supported(st.H, st.I, st.Hq, st.Hkv, st.D, st.n_layers, lm.N):
+        pytest.skip("qt_cp_step not supported on this device")
+    Lmax = 18
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+    for i, (R, pos) in enumerate([(8, p) for p in range(2, 16)] + [(3, 7), (8, 3), (2, 12)]):
+        x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+        ref = _chain(st, lm, x.clone(), x16.clone(), qkv0, [k.clone() for k in kc], [v.clone() for v in vc], R, Lmax,
+                     pos, dev)
+        logits = torch.full((R, lm.N), float("nan"), device=dev)
+        Kn.cp_step(st.layers, lm, x, qkv0, R, kc, vc, Lmax, pos, st.cos, st.sin, st.eps, logits, ws)
+        assert _rel(logits, ref) < 2e-2, (i, R, pos, _rel(logits, ref))
+    epoch = int(ws[4:8].view(torch.int32).item())
+    assert epoch == 17
+    assert int(ws[:4].view(torch.int32).item()) == 0
