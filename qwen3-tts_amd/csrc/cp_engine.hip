@@ -43,6 +43,9 @@ constexpr size_t OFF_PART = OFF_QKV + (size_t)NKV * MAXR * 512 * 8;   // [64 t][
 constexpr size_t OFF_X16 = OFF_PART + (size_t)64 * 4 * NKV * 32 * 8;  // [2][MAXR][H/2]
 constexpr size_t OFF_H = OFF_X16 + (size_t)2 * MAXR * (H / 2) * 8;    // [MAXR][I/2]
 constexpr size_t WS_BYTES = OFF_H + (size_t)MAXR * (I / 2) * 8;
+// optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
+// fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
+constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
 
 struct CEP {
   qt_cp_step_args a;
@@ -158,6 +161,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   u64* gx16 = (u64*)(ws + OFF_X16);
   u64* gh = (u64*)(ws + OFF_H);
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);  // (low word: the error flag)
+  float* dbg = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
   auto tagof = [&](int e) { return ep * NEDGE + (unsigned)e + 1u; };
   const int kvpos = p.const_pos, nc = kvpos;
   const int grp = lane / LPK, sub = lane % LPK;
@@ -360,6 +364,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         gm.each(lane, [&](int j, int d, float ov, float lv, float) { s.att[w][j * D + d] = f2bf(ov * __builtin_amdgcn_rcpf(lv)); });
       }
       __syncthreads();
+      if (dbg && l == 0 && cg == 0 && w < R)
+        for (int j = lane; j < NREP * D; j += 64) dbg[((size_t)3 * MAXR + w) * 4096 + h * NREP * D + j] = bf2f(s.att[w][j]);
       // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments f0, f0 + 1 of tile 2cg + tw
       {
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -406,6 +412,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
         for (int hp = 0; hp < NKV; ++hp) v += s.gath[hp][tid];
         s.xown[tid >> 4][tid & 15] += v;
+        if (dbg && l == 0 && 2 * qo + (tid >> 4) < R)
+          dbg[((size_t)0 * MAXR + 2 * qo + (tid >> 4)) * 4096 + 16 * to + (tid & 15)] = s.xown[tid >> 4][tid & 15];
       }
       __syncthreads();
       publish_x16(0, tagof(5 * l + 2));
@@ -425,12 +433,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         const f32x4_t v = red_sum(s, w * nw, nw, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int rr = lk * 4 + i;
-          const float g = v[i] * s.rs[rr];
+          const int rr = lk * 4 + i;  // MFMA rows 8..15 carry no batch row (zero A)
+          const float g = rr < MAXR ? v[i] * s.rs[rr] : 0.f;
           const float up = __shfl_xor(g, 8, 64);
           const float hv = silu_f(g) * up;
           const float hv2 = __shfl_xor(hv, 1, 64);  // column lm + 1's value (pairs 2p, 2p + 1)
-          if (lm < 8 && (lm & 1) == 0) s.hsw[w][rr][lm >> 1] = pack2bf(hv, hv2);
+          if (lm < 8 && (lm & 1) == 0 && rr < MAXR) s.hsw[w][rr][lm >> 1] = pack2bf(hv, hv2);
         }
       }
       __syncthreads();
@@ -438,6 +446,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         const int j = tid >> 5, rr = (tid >> 2) & 7, pp = tid & 3;
         const int tile = j == 0 ? b : b + NB;
         if (rr < R) st_g(gh + (size_t)rr * (I / 2) + tile * 4 + pp, s.hsw[j][rr][pp], tagof(5 * l + 3));
+        if (dbg && l == 0 && rr < R) {
+          dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp] = __uint_as_float(s.hsw[j][rr][pp] << 16);
+          dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp + 1] = __uint_as_float(s.hsw[j][rr][pp] & 0xFFFF0000u);
+        }
       }
     }
     // ------------------------------------------------------------------ P4: down tile `to` for rows 2qo, 2qo + 1
@@ -472,6 +484,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) v += s.red[ww][tid & 15][tid >> 4];
         s.xown[tid >> 4][tid & 15] += v;
+        if (dbg && l == 0 && 2 * qo + (tid >> 4) < R)
+          dbg[((size_t)2 * MAXR + 2 * qo + (tid >> 4)) * 4096 + 16 * to + (tid & 15)] = s.xown[tid >> 4][tid & 15];
       }
       __syncthreads();
       publish_x16(1, tagof(5 * l + 4));
@@ -517,6 +531,7 @@ bool cp_step_resident() {
 }  // namespace
 
 extern "C" long long qt_cp_step_ws_bytes(void) { return (long long)WS_BYTES; }
+extern "C" long long qt_cp_step_dbg_bytes(void) { return (long long)DBG_BYTES; }
 
 extern "C" int qt_cp_step_supported(int H_, int I_, int Hq, int Hkv, int D_, int n_layers, int V) {
   return H_ == H && I_ == I && Hq == NQ && Hkv == NKV && D_ == D && n_layers >= 1 && n_layers <= 6 && V % 16 == 0 &&

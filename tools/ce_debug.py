@@ -1,0 +1,89 @@
+"""Debug / A-B harness for qt_cp_step (the code-predictor step engine): engine vs the launch chain for 1..5 layers,
+repeated launches on one workspace and on fresh workspaces, launch counter and error flag after each launch.
+    python tools/ce_debug.py"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "qwen3-tts_amd"), os.path.join(REPO, "tests")]
+from test_gpu_cp_engine import _chain, _cp_stack, _inputs, _rel  # noqa: E402
+from qwen_tts import kernels as Kn  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    st, lm, g = _cp_stack(dev)
+    all_layers = list(st.layers)
+    Lmax = 18
+    for nl in (1, 2, 5):
+        st.layers = all_layers[:nl]
+        st.n_layers = nl
+        for R, pos in ((8, 2), (8, 9)):
+            x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+            ref = _chain(st, lm, x.clone(), x16.clone(), qkv0, [k.clone() for k in kc], [v.clone() for v in vc], R,
+                         Lmax, pos, dev)
+            ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+            res = []
+            for it in range(4):
+                fresh = it == 3
+                w = torch.zeros_like(ws) if fresh else ws
+                logits = torch.full((R, lm.N), float("nan"), device=dev)
+                Kn.cp_step(st.layers, lm, x, qkv0, R, [k.clone() for k in kc], [v.clone() for v in vc], Lmax, pos,
+                           st.cos, st.sin, st.eps, logits, w)
+                torch.cuda.synchronize()
+                ep = int(w[4:8].view(torch.int32).item())
+                err = int(w[:4].view(torch.int32).item())
+                res.append(logits)
+                print(f"nl={nl} R={R} pos={pos} launch {it}{' (fresh ws)' if fresh else ''}: rel vs chain "
+                      f"{_rel(logits, ref):.3e} epoch {ep} err {err} finite {bool(torch.isfinite(logits).all())} "
+                      f"same-as-first {bool(torch.equal(logits, res[0]))}", flush=True)
+    st.layers = all_layers
+    st.n_layers = len(all_layers)
+
+
+if __name__ == "__main__" and not os.environ.get("CE_LAYER0"):
+    main()
+
+
+def layer0():
+    """Layer-0 intermediates of the engine (workspace with the debug tail) vs the launch-chain kernels."""
+    from qwen_tts import _hip
+    dev = torch.device("cuda:0")
+    st, lm, g = _cp_stack(dev)
+    R, pos, Lmax = 8, 5, 18
+    x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+    L0 = st.layers[0]
+    # chain intermediates
+    att = torch.empty(R, st.Hq * st.D, dtype=torch.bfloat16, device=dev)
+    i32 = lambda t: torch.as_tensor(t, dtype=torch.int32, device=dev)  # noqa: E731
+    posv, rb, zero = i32([pos] * R), i32(range(R)), i32([0] * R)
+    Kn.decode_attention(qkv0, R, st.Hq, st.Hkv, st.D, L0.q_norm, L0.k_norm, st.eps, st.cos, st.sin, posv, rb, posv, zero,
+                        kc[0].clone(), vc[0].clone(), Lmax, att, const_pos=pos)
+    xa = x.clone()
+    xa16 = x16.clone()
+    Kn.gemm(att, L0.o, xa, R, st.Hq * st.D, st.H, epi=_hip.EPI_ADD, out2=xa16)
+    h = torch.empty(R, st.I, dtype=torch.bfloat16, device=dev)
+    Kn.gemm(xa16, L0.gu, h, R, st.H, st.I, rms=True, eps=st.eps, epi=_hip.EPI_SWIGLU)
+    xm = xa.clone()
+    Kn.gemm(h, L0.down, xm, R, st.I, st.H, epi=_hip.EPI_ADD)
+    n = Kn.cp_step_ws_bytes() + int(_hip.lib().qt_cp_step_dbg_bytes())
+    for it in range(3):
+        ws = torch.zeros(n, dtype=torch.uint8, device=dev)
+        logits = torch.full((R, lm.N), float("nan"), device=dev)
+        Kn.cp_step(st.layers[:1], lm, x, qkv0, R, [k.clone() for k in kc], [v.clone() for v in vc], Lmax, pos, st.cos,
+                   st.sin, st.eps, logits, ws)
+        torch.cuda.synchronize()
+        d = ws[Kn.cp_step_ws_bytes():].view(torch.float32).view(4, 8, 4096)
+        print(f"launch {it}: att rel {_rel(d[3, :R, :2048], att.float()):.3e}  x_attn rel {_rel(d[0, :R, :1024], xa):.3e}  "
+              f"h rel {_rel(d[1, :R, :3072], h.float()):.3e}  x_mlp rel {_rel(d[2, :R, :1024], xm):.3e}", flush=True)
+        for name, a, b in (("att", d[3, :R, :2048], att.float()), ("x_attn", d[0, :R, :1024], xa),
+                           ("h", d[1, :R, :3072], h.float())):
+            bad = ((a - b).abs() > 0.05 * b.abs().max()).nonzero()
+            if bad.numel():
+                print(f"   {name}: {bad.shape[0]} bad entries, first {bad[:8].tolist()}")
+
+
+if __name__ == "__main__" and os.environ.get("CE_LAYER0"):
+    layer0()
