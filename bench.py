@@ -323,15 +323,22 @@ def eng_wdt_bf16(tts):
     return tts.model.engine.wdt == torch.bfloat16
 
 
-def cpu_baseline(B, prompt, frames, threads):
-    """Oracle (CPU fp32 restatement of the reference) on a bounded sample of the same workload."""
+def cpu_baseline(B, prompt, frames, threads, preset="1.7b-customvoice"):
+    """Oracle (CPU fp32 restatement of the reference) on a bounded sample of the same workload, with the GPU run's own
+    seeded weights (qwen_tts.weights.synthetic on the CPU; the oracle's two extra codec input projections, which the
+    HIP path folds away, are seeded separately).  Cross-checked against the reference itself on this workload by
+    tests/golden/cpu_baseline_xval.py (profiles/*_cpu_baseline_xval.json, attached as `xval`)."""
     from oracle import CodecOracle, TalkerOracle, build_prompts, codec_param_specs, generate, load_preset
     from oracle.talker import talker_param_specs
+    from qwen_tts.weights import synthetic
     torch.set_num_threads(threads)
-    cfg, ccfg = load_preset("1.7b-customvoice")
+    cfg, ccfg = load_preset(preset)
+    cpu = torch.device("cpu")
+    W = synthetic(talker_param_specs(cfg), cpu)
+    cspecs = codec_param_specs(ccfg)
+    CW = synthetic([(n, s) for n, s in cspecs if not n.endswith("input_proj.weight")], cpu)
     g = torch.Generator().manual_seed(0)
-    W = {n: 0.02 * torch.randn(s, generator=g) for n, s in talker_param_specs(cfg)}
-    CW = {n: 0.02 * torch.randn(s, generator=g) for n, s in codec_param_specs(ccfg)}
+    CW.update({n: 0.02 * torch.randn(s, generator=g) for n, s in cspecs if n not in CW})
     o, co = TalkerOracle(cfg, W), CodecOracle(ccfg, CW)
     ids = [synth_ids(prompt, i) for i in range(B)]
     spk = ["vivian", "ryan", "serena", "aiden", "eric", "dylan", "sohee", "ono_anna"][:B]
@@ -343,10 +350,17 @@ def cpu_baseline(B, prompt, frames, threads):
         wav = co.decode(codes)
     dt = time.time() - t0
     audio = sum(w.shape[0] for w in wav) / 24000.0
+    xval = None
+    pdir = os.path.join(REPO, "profiles")
+    xs = sorted(f for f in os.listdir(pdir) if f.endswith("_cpu_baseline_xval.json"))
+    if xs:
+        j = json.load(open(os.path.join(pdir, xs[-1])))
+        xval = {"oracle_over_reference": round(j["oracle_over_reference"], 4), "threads": j["threads"],
+                "within_10pct": j["within_10pct"], "source": f"profiles/{xs[-1]} (container host, same workload shape)"}
     return dict(value=audio / dt, unit="audio-seconds/sec", cores=threads, threads=threads,
-                host_cpu_count=os.cpu_count(), kind="port",
-                sample=f"oracle fp32, 1.7B dims, B={B} x {prompt}-token prompts, {frames} frames + codec, {dt:.1f}s, "
-                       f"torch.set_num_threads({threads})")
+                host_cpu_count=os.cpu_count(), kind="port", xval=xval,
+                sample=f"oracle fp32, 1.7B dims, the GPU run's seeded weights, B={B} x {prompt}-token prompts, {frames} "
+                       f"sampled frames + codec, {dt:.1f}s, torch.set_num_threads({threads})")
 
 
 def _free_port() -> int:
@@ -454,6 +468,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=24)
+    ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--roofline", type=int, default=1)
     ap.add_argument("--workload", default="cv8", choices=["cv8", "vd64"],
                     help="cv8: configs[2] (default, weak scaling: 8 x 200-token CustomVoice utterances per GPU); vd64: "
@@ -582,8 +597,9 @@ def main():
                    "frac": round(pf["tflops"] / MFMA_BF16_PEAK_TFS, 4), "us_per_layer": round(pf["us_per_layer"], 1)}
     cpu = None
     if a.cpu_baseline and rank == 0 and world == 1:
-        # the box's CPU share (OMP_NUM_THREADS = 16 there); os.cpu_count() reports the whole host
-        cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, int(os.environ.get("OMP_NUM_THREADS", "16")))
+        # 8 threads: the reference's own published CPU figure and the cross-check use 8 (the box's CPU
+        # share is 16, os.cpu_count() reports the whole host)
+        cpu = cpu_baseline(B, a.prompt_tokens, a.cpu_frames, a.cpu_threads, a.preset)
     if rank == 0:
         per_utt_rtf = value / (B * world)
         out = {"metric": "audio-seconds/sec (RTF) + p50 first-packet latency, 1.7B @ batch 1/8, 1->8 GPU",

@@ -61,6 +61,11 @@ def full_cases():
         # frames (talker caches up to ~460 keys: the decode attention's length range in bench.py)
         "cv17_b2_long": dict(preset="1.7b-customvoice", idx=64, texts=[200, 150], languages=["english", "chinese"],
                              speakers=FULL_SPEAKERS[:2], non_streaming_mode=False, max_new_tokens=257),
+        # the long-cache route: 1.7B CustomVoice, 2 rows x 800 / 1000-token texts, NON-streaming (the whole text in the
+        # prompt), 48 frames -- talker caches of ~810-1060 keys, so every frame runs the split-KV decode attention
+        # (talker.attn_nsplit: 2 splits from 768 keys) and the refill-free frame graph of that split factor
+        "cv17_b2_longctx": dict(preset="1.7b-customvoice", idx=65, texts=[800, 1000], languages=["english", "auto"],
+                                speakers=FULL_SPEAKERS[2:4], non_streaming_mode=True, max_new_tokens=49),
         # configs[1]: 0.6B CustomVoice, 1 utterance of 120 text tokens, non-streaming (Identity small_to_mtp, M:1174)
         "cv06_b1_nonstream": dict(preset="0.6b-customvoice", idx=61, texts=[120], languages=["english"],
                                   speakers=["vivian"], non_streaming_mode=True, max_new_tokens=49),

@@ -91,15 +91,28 @@ def test_handoff_flag_raises_then_session_is_reused():
     assert all(int(s.cp.sc["ao_ws"][:4].view(torch.int32).item()) == 0 for s in ss)
     again, _ = m.generate(**kw)
     assert all(torch.equal(a, b) for a, b in zip(base, again))
-    # stream(): the flag set while frames decode is reported before the next chunk's audio is handed out
+    # the code-predictor step engine's own flag (qt_cp_step workspace)
+    ce = [s for s in ss if s.cp.ce_ws is not None]
+    if ce:
+        for s in ce:
+            s.cp.ce_ws[:4].view(torch.int32).fill_(1)
+        with pytest.raises(RuntimeError, match="hand-off timed out"):
+            m.generate(**kw)
+        assert all(int(s.cp.ce_ws[:4].view(torch.int32).item()) == 0 for s in ce)
+        again, _ = m.generate(**kw)
+        assert all(torch.equal(a, b) for a, b in zip(base, again))
+    # a streamed decode (decode_iter, as stream() drives it): the flag set while frames decode is reported at the next
+    # chunk boundary, before that chunk's frames are handed out
+    from qwen_tts.talker import GenParams
+    emb, mask, trail, pad = m.build_prompts(ids, ["english"], ["vivian"], None, True)
+    gp = GenParams(max_new_tokens=12, do_sample=False, subtalker_dosample=False, ignore_eos=True)
     chunks = 0
     with pytest.raises(RuntimeError, match="hand-off timed out"):
-        for _ in m.stream(**kw):
+        for sessions, frames, final in m.engine.decode_iter(emb, mask, trail, pad, gp, every=2, first=1):
             chunks += 1
-            for s in m.engine.all_sessions():
-                if s.busy and s.cp.sc.get("ao_ws") is not None:
-                    s.cp.sc["ao_ws"][:4].view(torch.int32).fill_(1)
+            for s in sessions:
+                s.cp.sc["ao_ws"][:4].view(torch.int32).fill_(1)
     assert chunks >= 1
-    assert HANDOFF_ERROR.startswith("qt_decode_attn_oproj")
+    assert "in-launch hand-off" in HANDOFF_ERROR
     again2, _ = m.generate(**kw)
     assert all(torch.equal(a, b) for a, b in zip(base, again2))

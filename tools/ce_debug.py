@@ -75,7 +75,7 @@ def layer0():
         Kn.cp_step(st.layers[:1], lm, x, qkv0, R, [k.clone() for k in kc], [v.clone() for v in vc], Lmax, pos, st.cos,
                    st.sin, st.eps, logits, ws)
         torch.cuda.synchronize()
-        d = ws[Kn.cp_step_ws_bytes():].view(torch.float32).view(4, 8, 4096)
+        d = ws[Kn.cp_step_ws_bytes():Kn.cp_step_ws_bytes() + 4 * 8 * 4096 * 4].view(torch.float32).view(4, 8, 4096)
         print(f"launch {it}: att rel {_rel(d[3, :R, :2048], att.float()):.3e}  x_attn rel {_rel(d[0, :R, :1024], xa):.3e}  "
               f"h rel {_rel(d[1, :R, :3072], h.float()):.3e}  x_mlp rel {_rel(d[2, :R, :1024], xm):.3e}", flush=True)
         for name, a, b in (("att", d[3, :R, :2048], att.float()), ("x_attn", d[0, :R, :1024], xa),
@@ -87,3 +87,54 @@ def layer0():
 
 if __name__ == "__main__" and os.environ.get("CE_LAYER0"):
     layer0()
+
+
+EVENTS = ["P1 wait", "x16(1) in", "qkv pub", "qkv in", "attn done", "part pub", "part in", "x16(0) pub", "x16(0) in",
+          "h pub", "h in", "x16(1) pub"]
+
+
+def stamps(R=8, reps=3):
+    """Per-phase timestamps (s_memrealtime, 10 ns) of 14 consecutive engine launches (cache positions 2..15), as a
+    frame issues them: per layer and event the median / max over blocks, microseconds from the launch's first block."""
+    from qwen_tts import _hip
+    import numpy as np
+    dev = torch.device("cuda:0")
+    st, lm, g = _cp_stack(dev)
+    Lmax = 18
+    x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+    nws = Kn.cp_step_ws_bytes()
+    n = nws + int(_hip.lib().qt_cp_step_dbg_bytes())
+    ws = torch.zeros(n, dtype=torch.uint8, device=dev)
+    logits = torch.empty(R, lm.N, device=dev)
+    dbg_off = nws + 4 * 8 * 4096 * 4
+    tot = []
+    for rep in range(reps):
+        for pos in range(2, 16):
+            Kn.cp_step(st.layers, lm, x, qkv0, R, kc, vc, Lmax, pos, st.cos, st.sin, st.eps, logits, ws)
+            torch.cuda.synchronize()
+            t = ws[dbg_off:].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64) * 0.01  # us
+            t0 = t[:, 0].min()
+            tot.append(t[:, 1].max() - t0)
+            if rep == reps - 1 and pos == 9:
+                print(f"launch at pos {pos}: first block start -> last block end {t[:, 1].max() - t0:.2f} us; start "
+                      f"spread {t[:, 0].max() - t0:.2f} us")
+                for l in range(st.n_layers):
+                    row = []
+                    for k, name in enumerate(EVENTS):
+                        v = t[:, 2 + 12 * l + k]
+                        if l == 0 and k < 3:
+                            continue
+                        row.append(f"{name} {np.median(v) - t0:6.2f}/{v.max() - t0:6.2f}")
+                    print(f"  layer {l}: " + " | ".join(row))
+                subs = {0: "P1 mfma", 1: "P1 red_put", 2: "P1 barrier", 3: "qkv stores", 4: "qkv drained",
+                        10: "P3 start", 11: "P3 dma waited", 12: "P3 mfma", 13: "P3 red_put", 14: "P3 barrier",
+                        15: "P3 swiglu", 16: "P3 barrier2", 17: "h stores", 18: "h drained", 20: "P4 wait start",
+                        21: "P4 staged", 22: "P4 barrier", 23: "P4 dma waited", 24: "P4 mfma+red", 25: "P4 barrier2"}
+                print("  layer 2 sub-phases: " + " | ".join(
+                    f"{n} {np.median(t[:, 64 + k]) - t0:6.2f}" for k, n in subs.items()))
+    print(f"kernel time (first start -> last end) over {len(tot)} launches: median {np.median(tot):.2f} us, "
+          f"min {np.min(tot):.2f}")
+
+
+if __name__ == "__main__" and os.environ.get("CE_STAMPS"):
+    stamps()
