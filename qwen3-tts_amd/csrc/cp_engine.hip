@@ -1,26 +1,31 @@
 // Code-predictor decode-step engine for gfx950: ONE persistent launch runs a whole code-predictor decode step -- the
 // 5 decoder layers (q/k/v projection -> q/k RMSNorm + RoPE + attention + o_proj + residual -> gate/up + SwiGLU ->
 // down + residual) and the final norm + lm_head[g] -- for up to 8 batch rows, where the launch chain issued ~21
-// dependent kernels per step (DESIGN §5, §11).  Replaces M:1250-1312 (Qwen3TTSTalkerCodePredictorModel.forward for one
+// dependent kernels per step (DESIGN §11).  Replaces M:1250-1312 (Qwen3TTSTalkerCodePredictorModel.forward for one
 // generated token, decoder layers M:961-1012, attention M:740-804 with q/k norm M:764-765) and M:1299 (lm_head[g]) for
 // every decode step of the code predictor (M:1671-1680); the token choice stays qt_sample.
 //
 // Structure (256 workgroups x 8 waves, one per CU, all resident -- the host checks the occupancy):
 //  * The residual stream is distributed: block (h, cg) OWNS x[rows 2q, 2q+1][cols 16t .. 16t+16) with t = 2cg + h/4,
 //    q = h % 4, in LDS, for the whole launch.  Only bf16 copies of x (the next GEMV's A operand) cross blocks.
-//  * Hand-offs are 8-byte {value, tag} granules written by one agent-scope (write-through) store each; the consumer
-//    re-reads a granule until its tag is this launch's edge tag (no flags, no fences, no resets: tag = epoch * 32 +
-//    edge + 1, the epoch a launch counter in the workspace, advanced by block 0 at the end of every launch once every
-//    block has read it).  Every all-to-all edge orders the buffer reuse of the next layer.
+//  * Bulk hand-offs (the q/k/v rows of a head, the x16 rows, the SwiGLU rows) follow the guide's R1 form: payload words
+//    stored write-through (agent scope, sc1), the storing wave drains them (s_waitcnt vmcnt(0)), then ONE flag word per
+//    producer block = the edge tag; a consumer's wave 0 polls the producers' flags, the block passes a barrier and reads
+//    the payload once with sc1 loads (no stale L1 / L2 line, no acquire fence).  The o_proj partials (2 KB per owner)
+//    are 8-byte {value, tag} granules (data = flag).  Tags: epoch * 32 + edge + 1, the epoch a launch counter in the
+//    workspace advanced by block 0 at the end of every launch (every block has read it by then) -- nothing is reset
+//    between launches.  Every all-to-all edge orders the buffer reuse of the next layer.
 //  * Every weight fragment a block multiplies in phase k + 1 is loaded into registers right after its phase-k MFMAs,
 //    before phase k's outputs are published and the edge into phase k + 1 is polled: the weight latency (Infinity
-//    Cache) overlaps the hand-off.
+//    Cache) overlaps the hand-off.  Addressing is buffer-resource based (SGPR base + 32-bit lane offsets), and the
+//    per-lane coordinates are re-derived from an opaque thread id every layer, so hipcc does not keep a 64-bit address
+//    per load site alive across the layer loop (that spilled ~30 registers).
 // Per layer: P1 q/k/v tile (h, cg) -> [QKV edge: the 32 blocks of head h] -> P2 head h's attention (every row) and its
 // K-slice of o_proj for 32 columns -> [partial edge: the 8 head blocks of a column group] -> residual add by the
-// owner -> [x16 edge, all-to-all] -> P3 gate/up tiles + SwiGLU -> [h edge: each owner's 2 rows] -> P4 down tile t
-// for the owner's 2 rows + residual -> [x16 edge] -> next layer (or the lm_head).  Numerics follow the launch chain:
-// bf16 weights and MFMA operands, fp32 accumulation, RMSNorm from the bf16 shadow's values, fp32 q/k/v, the attention
-// of attn_oproj_hs_k (q and keys as bf16 pairs, fp32 softmax), SwiGLU / attention outputs rounded to bf16.
+// owner -> [x16 edge, all-to-all] -> P3 gate/up tiles + SwiGLU -> [h edge: all-to-all] -> P4 down tile t for the
+// owner's 2 rows + residual -> [x16 edge] -> next layer (or the lm_head).  Numerics follow the launch chain: bf16
+// weights and MFMA operands, fp32 accumulation, RMSNorm from the bf16 shadow's values, fp32 q/k/v, the attention of
+// attn_oproj_hs_k (q and keys as bf16 pairs, fp32 softmax), SwiGLU / attention outputs rounded to bf16.
 #include "common.h"
 #include "attn_dev.h"
 #include <algorithm>
@@ -28,9 +33,10 @@
 namespace {
 
 typedef unsigned long long u64;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-constexpr int H = 1024, I = 3072, D = 128, NQ = 16, NKV = 8, NREP = 2, QKVW = (NQ + 2 * NKV) * D;
-constexpr int NB = 256, NT = 512, NW = 8, MAXR = 8;
+constexpr int H = 1024, I = 3072, D = 128, NQ = 16, NKV = 8, NREP = 2;
+constexpr int NB = 256, NW = 8, NT = NW * 64, MAXR = 8;
 constexpr int KTH = H / 32, KTI = I / 32, KTO = NQ * D / 32;  // k tiles: 32 / 96 / 64
 constexpr int LPK = D / 8, GPW = 64 / LPK, IC = 4;              // attention lane groups (attn_oproj_hs_k)
 constexpr int XLD = H + 8, HLD = I + 8, ALD = NREP * D + 8;       // LDS row strides (bf16)
@@ -38,20 +44,48 @@ constexpr int NEDGE = 32;                                         // tag slots p
 
 // workspace layout (bytes)
 constexpr size_t OFF_ERR = 0, OFF_EPOCH = 4;
-constexpr size_t OFF_QKV = 256;                                       // [NKV][MAXR][512] granules
-constexpr size_t OFF_PART = OFF_QKV + (size_t)NKV * MAXR * 512 * 8;   // [64 t][4 q][NKV][32]
-constexpr size_t OFF_X16 = OFF_PART + (size_t)64 * 4 * NKV * 32 * 8;  // [2][MAXR][H/2]
-constexpr size_t OFF_H = OFF_X16 + (size_t)2 * MAXR * (H / 2) * 8;    // [MAXR][I/2]
-constexpr size_t WS_BYTES = OFF_H + (size_t)MAXR * (I / 2) * 8;
+// The all-to-all edges (x16, SwiGLU rows) are written in NREPL replicas, one per XCD: a consumer polls and reads the
+// replica of its own XCD (blockIdx % 8 under round-robin placement -- any replica is correct, the choice only
+// spreads the traffic), so 32 blocks instead of 256 hammer one region's cache lines / memory channels (one shared
+// copy measured ~4-5 us per edge, contention-bound).
+constexpr int NREPL = 8;
+constexpr size_t OFF_FLAGS = 256;                                     // [FL_QKV: NB] + [NREPL][3][NB] producer flags
+constexpr int FL_X0 = 0, FL_X1 = 1, FL_H = 2;
+constexpr size_t REPL_FLAGS = (size_t)3 * NB * 4;                     // one replica's flag block (3 KB)
+constexpr size_t OFF_QKV = OFF_FLAGS + (size_t)NB * 4 + NREPL * REPL_FLAGS;  // [NKV][MAXR][512] fp32 payload
+constexpr size_t OFF_PART = OFF_QKV + (size_t)NKV * MAXR * 512 * 4;   // [64 t][4 q][NKV][32] granules
+constexpr size_t REPL_X16 = (size_t)2 * MAXR * (H / 2) * 4;           // [2][MAXR][H/2] bf16 pairs per replica
+constexpr size_t OFF_X16 = OFF_PART + (size_t)64 * 4 * NKV * 32 * 8;  // NREPL replicas
+constexpr size_t REPL_H = (size_t)MAXR * (I / 2) * 4;                 // [MAXR][I/2] bf16 pairs per replica
+constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;                  // NREPL replicas
+constexpr size_t WS_BYTES = OFF_H + NREPL * REPL_H;
 // optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
 // fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
 constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
+// ... and a workspace larger still records per-block phase timestamps (s_memrealtime, 100 MHz) after that:
+// [NB][64] u64 -- stamp 0 kernel start, 1 end, 2 + 12 l + k the layer-l events (tools/ce_debug.py names them)
+constexpr size_t STAMP_BYTES = (size_t)NB * 128 * 8;  // + [64, 128): sub-phase stamps of layer 2
 
 struct CEP {
   qt_cp_step_args a;
   int spin;
 };
 
+// ---- memory primitives
+QT_DEV rsrc_t mkr(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr int SC1 = 16;  // buffer-instruction cache policy: sc1 (agent-coherent, write-through)
+QT_DEV u32x4_t bld(rsrc_t r, unsigned off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0); }
+QT_DEV u32x4_t bld_c(rsrc_t r, unsigned off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SC1); }
+QT_DEV uint2 bld2_c(rsrc_t r, unsigned off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SC1);
+  return uint2{v[0], v[1]};
+}
+QT_DEV void bst_c(unsigned v, rsrc_t r, unsigned off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, SC1); }
+QT_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+QT_DEV unsigned ld_flag(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+QT_DEV void st_flag(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 QT_DEV u64 ld_g(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 QT_DEV void st_g(u64* p, unsigned v, unsigned tag) {
   __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -60,35 +94,46 @@ QT_DEV f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0,
                                                  0, 0);
 }
-QT_DEV u32x4_t ldw(const void* p) { return *(const u32x4_t*)p; }
-// weight fragment (n tile, k tile) of a pre-tiled bf16 matrix with `kt` k tiles: 1 KiB, lane l's 16 bytes
-QT_DEV const bf16_t* frag(const void* w, int nt, int ktile, int kt, int lane) {
-  return (const bf16_t*)w + ((size_t)nt * kt + ktile) * 512 + lane * 8;
-}
-// keep a loaded register alive and unmoved: the loads above are issued here, not sunk to their first use
+// byte offset of lane `lane`'s 16 bytes of weight fragment (n tile, k tile) of a pre-tiled bf16 matrix with kt k tiles
+QT_DEV unsigned fragoff(int nt, int ktile, int kt, int lane) { return ((unsigned)(nt * kt + ktile) << 10) + lane * 16; }
+// keep issued loads where they are (not sunk to their first use)
 #define CE_ISSUED() asm volatile("" ::: "memory")
+// LDS-DMA (global_load_lds_dwordx4, no VGPR staging): lane l's 16 bytes land at lds + 16 l; hipcc does not count it,
+// the issuing wave waits with its own s_waitcnt vmcnt before reading (vmcnt is in order, so every compiler wait on a
+// later load also covers it)
+QT_DEV void glds16(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+QT_DEV unsigned lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
+}
+QT_DEV void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// the phase's MFMAs are issued before the next phase's weight loads (so the two weight sets are never live together)
+#define CE_AFTER(acc) asm volatile("" : "+v"(acc)::"memory")
 
-// Re-read N consecutive granules until each carries `tag` (bounded; a give-up sets the sticky error flag and keeps
-// whatever was read).  Values are returned in v.
-template <int N>
-QT_DEV void poll_run(const u64* g, unsigned tag, unsigned (&v)[N], int spin, int* err) {
-  u64 x[N];
-#pragma unroll
-  for (int k = 0; k < N; ++k) x[k] = ld_g(g + k);
-  int spins = 0;
-  while (true) {
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < N; ++k) ok = ok && (unsigned)(x[k] >> 32) == tag;
-    if (ok) break;
-    if (++spins > spin) { atomicOr(err, 1); break; }
-    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-      if ((unsigned)(x[k] >> 32) != tag) x[k] = ld_g(g + k);
+// Wave 0 (the publishing wave) waits until the n (multiple of 4, <= 256) flag words at byte offset `off` all carry
+// `tag` -- one 16-byte sc1 load per lane per pass -- (bounded: a give-up sets the sticky error flag), then a block
+// barrier.
+QT_DEV void wait_flags(rsrc_t r, unsigned off, int n, unsigned tag, int spin, int* err) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (int spins = 0;; ++spins) {
+      bool ok = true;
+      if (lane * 4 < n) {
+        const u32x4_t v = bld_c(r, off + lane * 16);
+        ok = v[0] == tag && v[1] == tag && v[2] == tag && v[3] == tag;
+      }
+      if (__all(ok)) break;
+      if (spins > spin) {
+        if (lane == 0) atomicOr(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
   }
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = (unsigned)x[k];
+  __syncthreads();
 }
 
 struct Lds {
@@ -96,35 +141,36 @@ struct Lds {
     bf16_t xa[MAXR][XLD];  // x16 rows (all), the A operand of q/k/v, gate/up, lm_head
     bf16_t ha[2][HLD];     // the owner's two SwiGLU rows, the A operand of down
   } a;
-  float red[NW][64][4];                                   // per-wave MFMA partials
-  float rs[MAXR];                                         // 1 / rms per row
-  float rsp[NW];
-  float xown[2][16];                                      // the owned residual slice
-  float gath[NKV][32];                                    // the 8 head partials of the owned slice
-  unsigned hsw[2][MAXR][8];                               // SwiGLU outputs of the block's tiles (bf16 pairs)
+  float red[NW][64][4];                                        // per-wave MFMA partials
+  float rs[MAXR];                                              // 1 / rms per row
+  float xown[2][16];                                           // the owned residual slice
+  float gath[NKV][32];                                         // the 8 head partials of the owned slice
   __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];  // attention: q as bf16 pairs
   __attribute__((aligned(16))) unsigned kn2[NW][D / 2];        // the new key as bf16 pairs
   float vn[NW][D];                                             // the new value (bf16-rounded)
   __attribute__((aligned(16))) bf16_t att[NW][ALD];            // head h's attention output per row
 };
 
-// Stage the x16 edge (all rows, tag) into lds.a.xa and each row's 1 / rms (from the bf16 values, as the decode GEMV
-// computes it from the bf16 shadow).  Thread -> row tid / 64, pairs (tid % 64) * 8 .. + 8.
-QT_DEV void stage_x16(Lds& s, const u64* gx, unsigned tag, int R, float eps, int spin, int* err) {
-  const int tid = threadIdx.x, row = tid >> 6, p0 = (tid & 63) * 8;
-  unsigned v[8];
+// Stage the x16 edge (all rows) into lds.a.xa and each row's 1 / rms (from the bf16 values, as the decode GEMV computes
+// it from the bf16 shadow).  Thread -> row tid / 64, pairs (tid % 64) * 8 .. + 8: the payload read is spread over all
+// eight waves' memory queues.
+QT_DEV void stage_x16(Lds& s, rsrc_t gx, unsigned base, unsigned flag_off, unsigned tag, int R, float eps, int spin,
+                      int* err, int tid) {
+  const int row = tid >> 6, p0 = (tid & 63) * 8;
+  wait_flags(gx, flag_off, NB, tag, spin, err);
+  u32x4_t v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
   if (row < R) {
-    poll_run<8>(gx + (size_t)row * (H / 2) + p0, tag, v, spin, err);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = 0u;
+    const unsigned o = base + (unsigned)(row * (H / 2) + p0) * 4;
+    v0 = bld_c(gx, o);
+    v1 = bld_c(gx, o + 16);
   }
-  *(u32x4_t*)&s.a.xa[row][2 * p0] = u32x4_t{v[0], v[1], v[2], v[3]};
-  *(u32x4_t*)&s.a.xa[row][2 * p0 + 8] = u32x4_t{v[4], v[5], v[6], v[7]};
+  *(u32x4_t*)&s.a.xa[row][2 * p0] = v0;
+  *(u32x4_t*)&s.a.xa[row][2 * p0 + 8] = v1;
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float lo = __uint_as_float(v[k] << 16), hi = __uint_as_float(v[k] & 0xFFFF0000u);
+    const unsigned u = k < 4 ? v0[k] : v1[k - 4];
+    const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xFFFF0000u);
     ss += lo * lo + hi * hi;
   }
   ss = wave_sum_dpp(ss);  // wave == row
@@ -145,126 +191,173 @@ QT_DEV f32x4_t red_sum(const Lds& s, int w0, int nw, int lane) {
   }
   return v;
 }
+QT_DEV void red_put(Lds& s, int w, int lane, f32x4_t acc) {
+  s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
+}
 
 __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   const qt_cp_step_args& p = pk.a;
   __shared__ Lds s;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int lm = lane & 15, lk = lane >> 4;
   const int b = blockIdx.x, h = b >> 5, cg = b & 31;
   const int to = 2 * cg + (h >> 2), qo = h & 3;  // the owned residual slice: rows 2qo, 2qo + 1, cols 16to ..
   const int R = p.R;
   char* ws = (char*)p.ws;
   int* err = (int*)(ws + OFF_ERR);
-  u64* gqkv = (u64*)(ws + OFF_QKV);
+  unsigned* flags = (unsigned*)(ws + OFF_FLAGS);  // [0, NB): the q/k/v edge's flags
+  const int myrep = b % NREPL;                     // the replica this block reads (its XCD under round-robin placement)
+  auto fl_off = [&](int rp, int kind) { return (unsigned)(OFF_FLAGS + NB * 4 + rp * REPL_FLAGS + kind * NB * 4); };
   u64* gpart = (u64*)(ws + OFF_PART);
-  u64* gx16 = (u64*)(ws + OFF_X16);
-  u64* gh = (u64*)(ws + OFF_H);
+  const rsrc_t wsr = mkr(ws, (unsigned)WS_BYTES);  // payload regions, addressed by byte offset
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);  // (low word: the error flag)
   float* dbg = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
+  u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES + DBG_BYTES) + b * 128
+                                                                              : nullptr;
+#define CE_STAMP(k) \
+  if (stamps && threadIdx.x == 0) stamps[(k)] = __builtin_amdgcn_s_memrealtime();
+  CE_STAMP(0);
+#define CE_SUB(k) \
+  if (stamps && l == 2 && threadIdx.x == 0) stamps[64 + (k)] = __builtin_amdgcn_s_memrealtime();
   auto tagof = [&](int e) { return ep * NEDGE + (unsigned)e + 1u; };
   const int kvpos = p.const_pos, nc = kvpos;
-  const int grp = lane / LPK, sub = lane % LPK;
-  const int r = min(w, R - 1);  // attention: wave w = row w
-  const int vsel = min(grp, NREP + 1);
-  const int e0 = sub * 8, half = D / 2, ec = e0 % half;
-  const int slot = vsel * D + e0;  // this lane's 8 q/k/v values within head h's 512 (q0, q1, k, v)
-  const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
+  const int ntile3 = b < 128 ? 2 : 1;  // gate/up tiles: b and b + 256 for b < 128 (384 tiles)
+  // P1 tile of block (h, cg): head h's 32 q/k/v tiles (q: 16, k: 8, v: 8)
+  const int t1 = cg < 16 ? h * 16 + cg : (cg < 24 ? NQ * D / 16 + h * 8 + (cg - 16) : (NQ + NKV) * D / 16 + h * 8 + (cg - 24));
+  const unsigned kvstride = (unsigned)p.Lmax * D * 2;  // bytes per (row, kv head) cache slab
+  const unsigned kvbytes = (unsigned)R * NKV * kvstride;
 
-  // the owned residual slice
-  if (tid < 32) {
-    const int rr = 2 * qo + (tid >> 4);
-    s.xown[tid >> 4][tid & 15] = rr < R ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+  {  // the owned residual slice (wave 0)
+    const int tid = threadIdx.x;
+    if (tid < 32) {
+      const int rr = 2 * qo + (tid >> 4);
+      s.xown[tid >> 4][tid & 15] = rr < R ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+    }
   }
 
   // register-resident weights of the next phase (see the header)
-  u32x4_t w1[4];    // P1: q/k/v tile, k tiles 4w .. 4w + 3
+  u32x4_t w1[4];    // P1: q/k/v tile, k tiles 4w .. 4w + 3 (or the lm_head tile)
   u32x4_t w2[2];    // P2: o_proj, 2 fragments per wave
   u32x4_t w3[8];    // P3: gate/up, 4 (one tile) or 8 (two tiles) fragments per wave
   u32x4_t w4[12];   // P4: down tile `to`, k tiles 12w .. 12w + 11
   u32x4_t kq[IC], vq[IC];  // P2: cached keys / values of (row r, head h)
-  const int ntile3 = b < 3 * NB / 2 - NB ? 2 : 1;  // gate/up tiles: b and b + 256 for b < 128 (384 tiles)
-  const int t3 = ntile3 == 2 ? b + (w >> 2) * NB : b;
-  const int k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4, n3 = ntile3 == 2 ? 8 : 4;
-  // P1 tile of block (h, cg): head h's 32 q/k/v tiles (q: 16, k: 8, v: 8)
-  const int t1 = cg < 16 ? h * 16 + cg : (cg < 24 ? NQ * D / 16 + h * 8 + (cg - 16) : (NQ + NKV) * D / 16 + h * 8 + (cg - 24));
-  // P2: wave w multiplies o_proj fragments f0, f0 + 1 of tile (2cg + tw), head h's k tiles
-  const int f0 = w * 2, tw = f0 / 8, kt0 = f0 % 8;
 
-  auto load_p2 = [&](int l) {
+  // P2's loads: o_proj fragments f0, f0 + 1 of tile 2cg + f0 / 8 (head h's k tiles), cached keys / values of (row
+  // min(w, R - 1), head h) -- lane group grp owns keys grp, grp + 4, ... (clamped, masked in the math)
+  auto load_p2 = [&](int l, int tid) {
+    const int lane = tid & 63, w = tid >> 6, f0 = w * 2;
+    const rsrc_t wo = mkr(p.w_o[l], (unsigned)H * NQ * D * 2);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) w2[i] = ldw(frag(p.w_o[l], 2 * cg + tw, h * 8 + kt0 + i, KTO, lane));
-    const long long kvb = ((long long)r * NKV + h) * p.Lmax * D;
+    for (int i = 0; i < 2; ++i) w2[i] = bld(wo, fragoff(2 * cg + f0 / 8, h * 8 + f0 % 8 + i, KTO, lane));
+    const int r = min(w, R - 1), grp = lane / LPK, sub = lane % LPK;
+    const rsrc_t kr = mkr(p.k_cache[l], kvbytes), vr = mkr(p.v_cache[l], kvbytes);
+    const unsigned kvb = (unsigned)(r * NKV + h) * kvstride + sub * 16;
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
-      const int jj = min(c * GPW + grp, max(nc - 1, 0));
-      kq[c] = ldw((const bf16_t*)p.k_cache[l] + kvb + (long long)jj * D + sub * 8);
-      vq[c] = ldw((const bf16_t*)p.v_cache[l] + kvb + (long long)jj * D + sub * 8);
+      const unsigned o = kvb + (unsigned)min(c * GPW + grp, max(nc - 1, 0)) * D * 2;
+      kq[c] = bld(kr, o);
+      vq[c] = bld(vr, o);
     }
     CE_ISSUED();
   };
-  auto load_p3 = [&](int l) {
+  auto load_p3 = [&](int l, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const int t3 = ntile3 == 2 ? b + (w >> 2) * NB : b, k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4;
+    const int n3 = ntile3 == 2 ? 8 : 4;
+    const rsrc_t wg = mkr(p.w_gu[l], (unsigned)2 * I * H * 2);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w3[i] = ldw(frag(p.w_gu[l], t3, k3 + min(i, n3 - 1), KTH, lane));
+    for (int i = 0; i < 8; ++i) w3[i] = bld(wg, fragoff(t3, k3 + min(i, n3 - 1), KTH, lane));
     CE_ISSUED();
   };
-  auto load_p4 = [&](int l) {
+  auto load_p4 = [&](int l, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const rsrc_t wd = mkr(p.w_down[l], (unsigned)H * I * 2);
 #pragma unroll
-    for (int i = 0; i < 12; ++i) w4[i] = ldw(frag(p.w_down[l], to, w * 12 + i, KTI, lane));
+    for (int i = 0; i < 12; ++i) w4[i] = bld(wd, fragoff(to, w * 12 + i, KTI, lane));
     CE_ISSUED();
   };
-  auto load_p1 = [&](const void* wt, int tile) {
+  auto load_p1 = [&](const void* wt, unsigned bytes, int tile, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const rsrc_t wr = mkr(wt, bytes);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w1[i] = ldw(frag(wt, tile, w * 4 + i, KTH, lane));
+    for (int i = 0; i < 4; ++i) w1[i] = bld(wr, fragoff(tile, w * 4 + i, KTH, lane));
     CE_ISSUED();
   };
-
-  // publish the owned slice's bf16 copy (16 granules: 2 rows x 8 column pairs) to x16 buffer `buf`
-  auto publish_x16 = [&](int buf, unsigned tag) {
-    if (tid < 16) {
-      const int rr = tid >> 3, pp = tid & 7;
-      if (2 * qo + rr < R)
-        st_g(gx16 + ((size_t)buf * MAXR + 2 * qo + rr) * (H / 2) + 8 * to + pp,
-             pack2bf(s.xown[rr][2 * pp], s.xown[rr][2 * pp + 1]), tag);
+  // (wave 0, lane `lane`) publish the owned slice's bf16 copy (2 rows x 8 column pairs) to x16 buffer `buf` of every
+  // replica, drain, then the replicas' flags
+  auto publish_x16 = [&](int buf, unsigned tag, int lane) {
+    const int rr = (lane >> 3) & 1, pp = lane & 7, r0 = lane >> 4;
+    if (2 * qo + rr < R) {
+      const unsigned v = pack2bf(s.xown[rr][2 * pp], s.xown[rr][2 * pp + 1]);
+      const unsigned o = (unsigned)OFF_X16 + (unsigned)(((buf * MAXR + 2 * qo + rr) * (H / 2)) + 8 * to + pp) * 4;
+      bst_c(v, wsr, o + r0 * (unsigned)REPL_X16);
+      bst_c(v, wsr, o + (r0 + 4) * (unsigned)REPL_X16);
     }
+    drain_stores();
+    if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, FL_X0 + buf)) + b, tag);
   };
 
   const int L = p.n_layers;
-  load_p2(0);
+  load_p2(0, threadIdx.x);
   for (int l = 0; l < L; ++l) {
+    // per-lane coordinates from an opaque thread id: derived values are recomputed per layer, not kept alive
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, w = tid >> 6, lm = lane & 15, lk = lane >> 4;
+    // wave 0 publishes every edge: its weight loads are issued AFTER each publication, since its drain
+    // (s_waitcnt vmcnt(0)) would otherwise wait for them; the other waves issue theirs right after their MFMAs
+    const bool pubw = w == 0;
     // ------------------------------------------------------------------ P1: q/k/v projection (layers >= 1)
+    const int sb = 2 + 12 * l;
     if (l > 0) {
-      stage_x16(s, gx16 + (size_t)1 * MAXR * (H / 2), tagof(5 * (l - 1) + 4), R, p.eps, pk.spin, err);
+      CE_STAMP(sb + 0);
+      stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
+                tagof(5 * (l - 1) + 4), R, p.eps, pk.spin, err, tid);
+      CE_STAMP(sb + 1);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, R), w1[i], acc);
-      load_p2(l);
-      s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
+      CE_AFTER(acc);
+      CE_SUB(0);
+      if (!pubw) load_p2(l, tid);
+      red_put(s, w, lane, acc);
       __syncthreads();
-      if (w == 0) {
+      CE_SUB(2);
+      if (pubw) {
         const f32x4_t v = red_sum(s, 0, NW, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rr = lk * 4 + i;
-          if (rr < R) st_g(gqkv + ((size_t)h * MAXR + rr) * 512 + cg * 16 + lm, __float_as_uint(v[i] * s.rs[rr]),
-                           tagof(5 * l));
+          if (rr < R)
+            bst_c(__float_as_uint(v[i] * s.rs[rr]), wsr,
+                  (unsigned)OFF_QKV + (unsigned)((h * MAXR + rr) * 512 + cg * 16 + lm) * 4);
         }
+        CE_SUB(3);
+        drain_stores();
+        CE_SUB(4);
+        if (lane == 0) st_flag(flags + b, tagof(5 * l));
+        load_p2(l, tid);
       }
+      CE_STAMP(sb + 2);
     }
     // ------------------------------------------------------------------ P2: attention of head h + o_proj K-slice
     {
+      const int r = min(w, R - 1);  // wave w = row w
+      const int grp = lane / LPK, sub = lane % LPK;
+      const int vsel = min(grp, NREP + 1);
+      const int e0 = sub * 8, half = D / 2, ec = e0 % half;
       float xv[8];
       if (l == 0) {
+        const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
         load8f(p.qkv0 + (long long)r * p.ldq + (long long)hh * D + e0, xv);
       } else {
-        unsigned v[8];
-        poll_run<8>(gqkv + ((size_t)h * MAXR + r) * 512 + slot, tagof(5 * l), v, pk.spin, err);
+        wait_flags(wsr, (unsigned)OFF_FLAGS + h * 32 * 4, 32, tagof(5 * l), pk.spin, err);  // head h's 32 q/k/v tiles
+        const unsigned o = (unsigned)OFF_QKV + (unsigned)((h * MAXR + r) * 512 + vsel * D + e0) * 4;
+        const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) xv[k] = __uint_as_float(v[k]);
+        for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
       }
+      CE_STAMP(sb + 3);
       float nwv[8], cv[8], sv[8];
-      const float* nwp = vsel < NREP ? p.q_norm[l] : p.k_norm[l];
-      load8f(nwp + e0, nwv);
+      load8f((vsel < NREP ? p.q_norm[l] : p.k_norm[l]) + e0, nwv);
       load8f(p.cos_tab + (long long)kvpos * half + ec, cv);
       load8f(p.sin_tab + (long long)kvpos * half + ec, sv);
       {  // q/k RMSNorm + RoPE (branch-free over the lane groups; the v group's result is discarded)
@@ -341,7 +434,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           const float en = grp == 0 ? exp2_hw(dn[j] - mn) : 0.f;
           unsigned epk[IC / 2];
 #pragma unroll
-          for (int pr = 0; pr < IC / 2; ++pr) epk[pr] = pack2bf_rne(exp2_hw(dd[j][2 * pr] - mn), exp2_hw(dd[j][2 * pr + 1] - mn));
+          for (int pr = 0; pr < IC / 2; ++pr)
+            epk[pr] = pack2bf_rne(exp2_hw(dd[j][2 * pr] - mn), exp2_hw(dd[j][2 * pr + 1] - mn));
           float ls = en;
 #pragma unroll
           for (int pr = 0; pr < IC / 2; ++pr)
@@ -364,29 +458,32 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         gm.each(lane, [&](int j, int d, float ov, float lv, float) { s.att[w][j * D + d] = f2bf(ov * __builtin_amdgcn_rcpf(lv)); });
       }
       __syncthreads();
+      CE_STAMP(sb + 4);
       if (dbg && l == 0 && cg == 0 && w < R)
         for (int j = lane; j < NREP * D; j += 64) dbg[((size_t)3 * MAXR + w) * 4096 + h * NREP * D + j] = bf2f(s.att[w][j]);
-      // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments f0, f0 + 1 of tile 2cg + tw
+      // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments 2w, 2w + 1 of tile 2cg + w / 4
       {
+        const int kt0 = (2 * w) % 8;
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const u32x4_t av = lm < NW ? *(const u32x4_t*)&s.att[lm][(kt0 + i) * 32 + lk * 8] : u32x4_t{0u, 0u, 0u, 0u};
           acc = mfma(av, w2[i], acc);
         }
-        load_p3(l);
-        s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
-      }
-      // the new k / v of (row w, head h) into the caches (one column group appends)
-      if (cg == 0 && w < R && lane < D / 2) {
-        const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
-        ((unsigned*)p.k_cache[l])[o / 2 + lane] = s.kn2[w][lane];
-        ((bf16_t*)p.v_cache[l])[o + lane] = f2bf(s.vn[w][lane]);
-        ((bf16_t*)p.v_cache[l])[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
+        CE_AFTER(acc);
+        if (!pubw) load_p3(l, tid);
+        red_put(s, w, lane, acc);
+        // the new k / v of (row w, head h) into the caches (one column group appends)
+        if (cg == 0 && w < R && lane < D / 2) {
+          const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
+          ((unsigned*)p.k_cache[l])[o / 2 + lane] = s.kn2[w][lane];
+          ((bf16_t*)p.v_cache[l])[o + lane] = f2bf(s.vn[w][lane]);
+          ((bf16_t*)p.v_cache[l])[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
+        }
       }
       __syncthreads();
-      // row rr's partial for column c (thread (rr, c < 32)): the tile's 4 waves summed in wave order -> the owner of
-      // (tile 2cg + c / 16, row pair rr / 2)
+      // row rr's partial for column c (thread (rr, c < 32), waves 0-3): the tile's 4 waves summed in wave order -> the
+      // owner of (tile 2cg + c / 16, row pair rr / 2), as granules (data = flag: no drain)
       if (tid < MAXR * 32) {
         const int rr = tid >> 5, c = tid & 31, tt = c >> 4, cc = c & 15;
         float v = 0.f;
@@ -396,78 +493,108 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           st_g(gpart + ((((size_t)(2 * cg + tt) * 4 + (rr >> 1)) * NKV + h) * 32 + (rr & 1) * 16 + cc),
                __float_as_uint(v), tagof(5 * l + 1));
       }
+      CE_STAMP(sb + 5);
     }
     // ------------------------------------------------------------------ residual add by the owner, x16 edge
     {
-      if (tid < NKV * 32) {
+      if (tid < NKV * 32) {  // the 8 head partials of the owned slice (granules, polled; waves 0-3)
         const int hp = tid >> 5, sl = tid & 31;
-        unsigned v[1] = {0u};
-        if (2 * qo + (sl >> 4) < R)
-          poll_run<1>(gpart + ((((size_t)to * 4 + qo) * NKV + hp) * 32 + sl), tagof(5 * l + 1), v, pk.spin, err);
-        s.gath[hp][sl] = __uint_as_float(v[0]);
+        unsigned v = 0u;
+        if (2 * qo + (sl >> 4) < R) {
+          const u64* g = gpart + ((((size_t)to * 4 + qo) * NKV + hp) * 32 + sl);
+          const unsigned want = tagof(5 * l + 1);
+          u64 x = ld_g(g);
+          for (int spins = 0; (unsigned)(x >> 32) != want; ++spins) {
+            if (spins > pk.spin) { atomicOr(err, 1); break; }
+            __builtin_amdgcn_s_sleep(1);
+            x = ld_g(g);
+          }
+          v = (unsigned)x;
+        }
+        s.gath[hp][sl] = __uint_as_float(v);
       }
       __syncthreads();
-      if (tid < 32) {
-        float v = 0.f;
+      CE_STAMP(sb + 6);
+      if (pubw) {
+        if (lane < 32) {
+          float v = 0.f;
 #pragma unroll
-        for (int hp = 0; hp < NKV; ++hp) v += s.gath[hp][tid];
-        s.xown[tid >> 4][tid & 15] += v;
-        if (dbg && l == 0 && 2 * qo + (tid >> 4) < R)
-          dbg[((size_t)0 * MAXR + 2 * qo + (tid >> 4)) * 4096 + 16 * to + (tid & 15)] = s.xown[tid >> 4][tid & 15];
+          for (int hp = 0; hp < NKV; ++hp) v += s.gath[hp][lane];  // head order
+          s.xown[lane >> 4][lane & 15] += v;
+          if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
+            dbg[((size_t)0 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
+        }
+        publish_x16(0, tagof(5 * l + 2), lane);  // (the wave's own LDS writes above are complete: one wave, in order)
+        load_p3(l, tid);
       }
-      __syncthreads();
-      publish_x16(0, tagof(5 * l + 2));
+      CE_STAMP(sb + 7);
     }
     // ------------------------------------------------------------------ P3: gate/up + SwiGLU
     {
-      stage_x16(s, gx16, tagof(5 * l + 2), R, p.eps, pk.spin, err);
+      stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16), fl_off(myrep, FL_X0), tagof(5 * l + 2), R, p.eps, pk.spin,
+                err, tid);
+      CE_STAMP(sb + 8);
+      const int k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4, n3 = ntile3 == 2 ? 8 : 4;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (i < n3) acc = mfma(afrag_x(s, lm, lk, k3 + i, R), w3[i], acc);
-      load_p4(l);
-      s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
+      CE_AFTER(acc);
+      CE_SUB(12);
+      if (!pubw) load_p4(l, tid);
+      red_put(s, w, lane, acc);
       __syncthreads();
-      if (w < ntile3) {  // wave j finishes tile j: column lm (gate lm < 8, up lm + 8), rows lk*4 .. + 3
-        const int nw = ntile3 == 2 ? 4 : 8;
-        const f32x4_t v = red_sum(s, w * nw, nw, lane);
+      CE_SUB(14);
+      if (pubw) {  // SwiGLU of (tile j, row rr, column pair pp) from the partials, every replica, drain, flags
+        const int j = lane >> 5, rr = (lane >> 2) & 7, pp = lane & 3;
+        const int tile = j == 0 ? b : b + NB, nw = ntile3 == 2 ? 4 : 8;
+        const bool mine = lane < ntile3 * MAXR * 4 && rr < R;
+        if (mine) {
+          const int ml = (rr >> 2) * 16 + 2 * pp, e = rr & 3;  // MFMA lane of (row rr, gate column 2pp)
+          float g0 = 0.f, g1 = 0.f, u0 = 0.f, u1 = 0.f;
+          for (int ww = j * nw; ww < j * nw + nw; ++ww) {
+            g0 += s.red[ww][ml][e]; g1 += s.red[ww][ml + 1][e];
+            u0 += s.red[ww][ml + 8][e]; u1 += s.red[ww][ml + 9][e];
+          }
+          const float rsv = s.rs[rr];
+          const float h0 = silu_f(g0 * rsv) * (u0 * rsv), h1 = silu_f(g1 * rsv) * (u1 * rsv);
+          const unsigned hv = pack2bf(h0, h1);
+          const unsigned o = (unsigned)OFF_H + (unsigned)(rr * (I / 2) + tile * 4 + pp) * 4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int rr = lk * 4 + i;  // MFMA rows 8..15 carry no batch row (zero A)
-          const float g = rr < MAXR ? v[i] * s.rs[rr] : 0.f;
-          const float up = __shfl_xor(g, 8, 64);
-          const float hv = silu_f(g) * up;
-          const float hv2 = __shfl_xor(hv, 1, 64);  // column lm + 1's value (pairs 2p, 2p + 1)
-          if (lm < 8 && (lm & 1) == 0 && rr < MAXR) s.hsw[w][rr][lm >> 1] = pack2bf(hv, hv2);
+          for (int rp = 0; rp < NREPL; ++rp) bst_c(hv, wsr, o + rp * (unsigned)REPL_H);
+          if (dbg && l == 0) {
+            dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp] = __uint_as_float(hv << 16);
+            dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp + 1] = __uint_as_float(hv & 0xFFFF0000u);
+          }
         }
+        CE_SUB(17);
+        drain_stores();
+        CE_SUB(18);
+        if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, FL_H)) + b, tagof(5 * l + 3));
+        load_p4(l, tid);
       }
-      __syncthreads();
-      if (tid < ntile3 * MAXR * 4) {
-        const int j = tid >> 5, rr = (tid >> 2) & 7, pp = tid & 3;
-        const int tile = j == 0 ? b : b + NB;
-        if (rr < R) st_g(gh + (size_t)rr * (I / 2) + tile * 4 + pp, s.hsw[j][rr][pp], tagof(5 * l + 3));
-        if (dbg && l == 0 && rr < R) {
-          dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp] = __uint_as_float(s.hsw[j][rr][pp] << 16);
-          dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp + 1] = __uint_as_float(s.hsw[j][rr][pp] & 0xFFFF0000u);
-        }
-      }
+      CE_STAMP(sb + 9);
     }
     // ------------------------------------------------------------------ P4: down tile `to` for rows 2qo, 2qo + 1
     {
+      CE_SUB(20);
+      wait_flags(wsr, fl_off(myrep, FL_H), NB, tagof(5 * l + 3), pk.spin, err);
+      CE_STAMP(sb + 10);
       {  // the owner's two SwiGLU rows: thread -> row tid / 256, pairs (tid % 256) * 6 .. + 5
         const int rr = tid >> 8, p0 = (tid & 255) * 6;
-        unsigned v[6];
+        uint2 v[3] = {{0u, 0u}, {0u, 0u}, {0u, 0u}};
         if (2 * qo + rr < R) {
-          poll_run<6>(gh + (size_t)(2 * qo + rr) * (I / 2) + p0, tagof(5 * l + 3), v, pk.spin, err);
-        } else {
+          const unsigned o = (unsigned)(OFF_H + myrep * REPL_H) + (unsigned)((2 * qo + rr) * (I / 2) + p0) * 4;
 #pragma unroll
-          for (int k = 0; k < 6; ++k) v[k] = 0u;
+          for (int k = 0; k < 3; ++k) v[k] = bld2_c(wsr, o + 8 * k);
         }
-        unsigned* hrow = (unsigned*)&s.a.ha[rr][0];
+        uint2* hrow = (uint2*)&s.a.ha[rr][2 * p0];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) hrow[p0 + k] = v[k];
+        for (int k = 0; k < 3; ++k) hrow[k] = v[k];
       }
+      CE_SUB(21);
       __syncthreads();
+      CE_SUB(22);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 12; ++i) {
@@ -475,43 +602,56 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         const u32x4_t av = lm < 2 ? *(const u32x4_t*)&s.a.ha[lm][kt * 32 + lk * 8] : u32x4_t{0u, 0u, 0u, 0u};
         acc = mfma(av, w4[i], acc);
       }
-      if (l + 1 < L) load_p1(p.w_qkv[l + 1], t1);
-      else if (b < p.V / 16) load_p1(p.w_lm, b);
-      s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
+      CE_AFTER(acc);
+      auto next_w1 = [&]() {
+        if (l + 1 < L) load_p1(p.w_qkv[l + 1], (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, tid);
+        else if (b < p.V / 16) load_p1(p.w_lm, (unsigned)p.V * H * 2, b, tid);
+      };
+      if (!pubw) next_w1();
+      red_put(s, w, lane, acc);
       __syncthreads();
-      if (tid < 32) {  // (row tid / 16, column tid % 16) = MFMA row tid / 16 of lane tid % 16
-        float v = 0.f;
+      CE_SUB(25);
+      if (pubw) {
+        if (lane < 32) {  // (row lane / 16, column lane % 16) = MFMA row lane / 16 of MFMA lane lane % 16
+          float v = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) v += s.red[ww][tid & 15][tid >> 4];
-        s.xown[tid >> 4][tid & 15] += v;
-        if (dbg && l == 0 && 2 * qo + (tid >> 4) < R)
-          dbg[((size_t)2 * MAXR + 2 * qo + (tid >> 4)) * 4096 + 16 * to + (tid & 15)] = s.xown[tid >> 4][tid & 15];
+          for (int ww = 0; ww < NW; ++ww) v += s.red[ww][lane & 15][lane >> 4];
+          s.xown[lane >> 4][lane & 15] += v;
+          if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
+            dbg[((size_t)2 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
+        }
+        publish_x16(1, tagof(5 * l + 4), lane);
+        next_w1();
       }
-      __syncthreads();
-      publish_x16(1, tagof(5 * l + 4));
+      CE_STAMP(sb + 11);
     }
   }
   // -------------------------------------------------------------------- final norm + lm_head[g] (tiles 0 .. V/16)
-  stage_x16(s, gx16 + (size_t)1 * MAXR * (H / 2), tagof(5 * (L - 1) + 4), R, p.eps, pk.spin, err);
-  if (b < p.V / 16) {
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lm = lane & 15, lk = lane >> 4;
+    stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
+              tagof(5 * (L - 1) + 4), R, p.eps, pk.spin, err, tid);
+    if (b < p.V / 16) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, R), w1[i], acc);
-    s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
-    __syncthreads();
-    if (w == 0) {
-      const f32x4_t v = red_sum(s, 0, NW, lane);
+      for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, R), w1[i], acc);
+      red_put(s, w, lane, acc);
+      __syncthreads();
+      if (w == 0) {
+        const f32x4_t v = red_sum(s, 0, NW, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = lk * 4 + i;
-        if (rr < R) p.logits[(long long)rr * p.ldl + b * 16 + lm] = v[i] * s.rs[rr];
+        for (int i = 0; i < 4; ++i) {
+          const int rr = lk * 4 + i;
+          if (rr < R) p.logits[(long long)rr * p.ldl + b * 16 + lm] = v[i] * s.rs[rr];
+        }
       }
     }
+    // the launch counter: every block read it before its first publication, and block 0 has consumed an edge from
+    // every block by now
+    if (b == 0 && tid == 0)
+      __hip_atomic_store((unsigned*)(ws + OFF_EPOCH), ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CE_STAMP(1);
   }
-  // the launch counter: every block read it before its first publication, and block 0 has consumed an edge from every
-  // block by now
-  if (b == 0 && tid == 0)
-    __hip_atomic_store((unsigned*)(ws + OFF_EPOCH), ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 bool cp_step_resident() {
@@ -531,7 +671,7 @@ bool cp_step_resident() {
 }  // namespace
 
 extern "C" long long qt_cp_step_ws_bytes(void) { return (long long)WS_BYTES; }
-extern "C" long long qt_cp_step_dbg_bytes(void) { return (long long)DBG_BYTES; }
+extern "C" long long qt_cp_step_dbg_bytes(void) { return (long long)(DBG_BYTES + STAMP_BYTES); }
 
 extern "C" int qt_cp_step_supported(int H_, int I_, int Hq, int Hkv, int D_, int n_layers, int V) {
   return H_ == H && I_ == I && Hq == NQ && Hkv == NKV && D_ == D && n_layers >= 1 && n_layers <= 6 && V % 16 == 0 &&
@@ -542,6 +682,7 @@ extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
   if (!a || a->R < 1 || a->R > MAXR || a->n_layers < 1 || a->n_layers > 6) return QT_ERR_SHAPE;
   if (a->const_pos < 1 || a->const_pos > IC * GPW || a->const_pos >= a->Lmax) return QT_ERR_SHAPE;
   if (a->V % 16 || a->V / 16 > NB || a->V <= 0) return QT_ERR_SHAPE;
+  if ((long long)a->R * NKV * a->Lmax * D * 2 >= (1ll << 31)) return QT_ERR_SHAPE;  // 32-bit buffer offsets
   if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->x || !a->qkv0 || !a->logits || !a->w_lm || !a->cos_tab ||
       !a->sin_tab)
     return QT_ERR_ARG;
