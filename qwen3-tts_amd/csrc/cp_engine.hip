@@ -111,6 +111,8 @@ QT_DEV unsigned lds_u32(const void* p) {
 }
 QT_DEV void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // the phase's MFMAs are issued before the next phase's weight loads (so the two weight sets are never live together)
+// all four A fragments read (one LDS wait) before the first MFMA, instead of a wait per MFMA
+QT_DEV void pin4(u32x4_t* a) { asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3])); }
 #define CE_AFTER(acc) asm volatile("" : "+v"(acc)::"memory")
 
 // Wave 0 (the publishing wave) waits until the n (multiple of 4, <= 256) flag words at byte offset `off` all carry
@@ -136,6 +138,16 @@ QT_DEV void wait_flags(rsrc_t r, unsigned off, int n, unsigned tag, int spin, in
   __syncthreads();
 }
 
+// the eight per-layer pointer arrays of qt_cp_step_args, in their declaration order (contiguous: read as one table)
+enum { PT_QKV, PT_O, PT_GU, PT_DOWN, PT_QN, PT_KN, PT_KC, PT_VC };
+static_assert(offsetof(qt_cp_step_args, w_o) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_O, "pointer table");
+static_assert(offsetof(qt_cp_step_args, w_gu) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_GU, "pointer table");
+static_assert(offsetof(qt_cp_step_args, w_down) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_DOWN, "pointer table");
+static_assert(offsetof(qt_cp_step_args, q_norm) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_QN, "pointer table");
+static_assert(offsetof(qt_cp_step_args, k_norm) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_KN, "pointer table");
+static_assert(offsetof(qt_cp_step_args, k_cache) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_KC, "pointer table");
+static_assert(offsetof(qt_cp_step_args, v_cache) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_VC, "pointer table");
+
 struct Lds {
   union {
     bf16_t xa[MAXR][XLD];  // x16 rows (all), the A operand of q/k/v, gate/up, lm_head
@@ -144,6 +156,8 @@ struct Lds {
   float red[NW][64][4];                                        // per-wave MFMA partials
   float rs[MAXR];                                              // 1 / rms per row
   float xown[2][16];                                           // the owned residual slice
+  __attribute__((aligned(16))) bf16_t zero[32];                // the A rows past the batch (MFMA rows >= R)
+  const void* ptab[8][8];  // per-layer pointers [PT_*][layer]: one LDS read instead of a scalar kernarg miss per use
   float gath[NKV][32];                                         // the 8 head partials of the owned slice
   __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];  // attention: q as bf16 pairs
   __attribute__((aligned(16))) unsigned kn2[NW][D / 2];        // the new key as bf16 pairs
@@ -180,7 +194,7 @@ QT_DEV void stage_x16(Lds& s, rsrc_t gx, unsigned base, unsigned flag_off, unsig
 
 // A fragment of MFMA row lm (batch row; rows >= R zero) at k tile kt from the staged x16 rows
 QT_DEV u32x4_t afrag_x(const Lds& s, int lm, int lk, int kt, int R) {
-  return lm < R ? *(const u32x4_t*)&s.a.xa[lm][kt * 32 + lk * 8] : u32x4_t{0u, 0u, 0u, 0u};
+  return *(const u32x4_t*)(lm < R ? &s.a.xa[lm][kt * 32 + lk * 8] : &s.zero[lk * 8]);
 }
 
 // Sum the per-wave partials of waves [w0, w0 + nw) for lane `lane` (fixed wave order)
@@ -225,13 +239,25 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   const unsigned kvstride = (unsigned)p.Lmax * D * 2;  // bytes per (row, kv head) cache slab
   const unsigned kvbytes = (unsigned)R * NKV * kvstride;
 
-  {  // the owned residual slice (wave 0)
+  {  // the owned residual slice (wave 0), the zero A row, the per-layer pointer table (wave 1)
     const int tid = threadIdx.x;
     if (tid < 32) {
       const int rr = 2 * qo + (tid >> 4);
       s.xown[tid >> 4][tid & 15] = rr < R ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+    } else if (tid < 48) {
+      ((unsigned*)s.zero)[tid - 32] = 0u;
+    } else if (tid >= 64 && tid < 128) {
+      (&s.ptab[0][0])[tid - 64] = (&p.w_qkv[0])[tid - 64];
     }
+    __syncthreads();
   }
+  // a per-layer pointer, wave-uniform (SGPRs)
+  auto lp = [&](int k, int l) -> const void* {
+    const u64 v = (u64)s.ptab[k][l];
+    // (readfirstlane returns int: widen through unsigned, or the low word's sign bit would smear into the high word)
+    return (const void*)(((u64)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                         (u64)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)v));
+  };
 
   // register-resident weights of the next phase (see the header)
   u32x4_t w1[4];    // P1: q/k/v tile, k tiles 4w .. 4w + 3 (or the lm_head tile)
@@ -244,11 +270,11 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   // min(w, R - 1), head h) -- lane group grp owns keys grp, grp + 4, ... (clamped, masked in the math)
   auto load_p2 = [&](int l, int tid) {
     const int lane = tid & 63, w = tid >> 6, f0 = w * 2;
-    const rsrc_t wo = mkr(p.w_o[l], (unsigned)H * NQ * D * 2);
+    const rsrc_t wo = mkr(lp(PT_O, l), (unsigned)H * NQ * D * 2);
 #pragma unroll
     for (int i = 0; i < 2; ++i) w2[i] = bld(wo, fragoff(2 * cg + f0 / 8, h * 8 + f0 % 8 + i, KTO, lane));
     const int r = min(w, R - 1), grp = lane / LPK, sub = lane % LPK;
-    const rsrc_t kr = mkr(p.k_cache[l], kvbytes), vr = mkr(p.v_cache[l], kvbytes);
+    const rsrc_t kr = mkr(lp(PT_KC, l), kvbytes), vr = mkr(lp(PT_VC, l), kvbytes);
     const unsigned kvb = (unsigned)(r * NKV + h) * kvstride + sub * 16;
 #pragma unroll
     for (int c = 0; c < IC; ++c) {
@@ -262,14 +288,14 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
     const int lane = tid & 63, w = tid >> 6;
     const int t3 = ntile3 == 2 ? b + (w >> 2) * NB : b, k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4;
     const int n3 = ntile3 == 2 ? 8 : 4;
-    const rsrc_t wg = mkr(p.w_gu[l], (unsigned)2 * I * H * 2);
+    const rsrc_t wg = mkr(lp(PT_GU, l), (unsigned)2 * I * H * 2);
 #pragma unroll
     for (int i = 0; i < 8; ++i) w3[i] = bld(wg, fragoff(t3, k3 + min(i, n3 - 1), KTH, lane));
     CE_ISSUED();
   };
   auto load_p4 = [&](int l, int tid) {
     const int lane = tid & 63, w = tid >> 6;
-    const rsrc_t wd = mkr(p.w_down[l], (unsigned)H * I * 2);
+    const rsrc_t wd = mkr(lp(PT_DOWN, l), (unsigned)H * I * 2);
 #pragma unroll
     for (int i = 0; i < 12; ++i) w4[i] = bld(wd, fragoff(to, w * 12 + i, KTI, lane));
     CE_ISSUED();
@@ -312,13 +338,17 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
                 tagof(5 * (l - 1) + 4), R, p.eps, pk.spin, err, tid);
       CE_STAMP(sb + 1);
+      u32x4_t af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = afrag_x(s, lm, lk, w * 4 + i, R);
+      pin4(af);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, R), w1[i], acc);
+      for (int i = 0; i < 4; ++i) acc = mfma(af[i], w1[i], acc);
       CE_AFTER(acc);
       CE_SUB(0);
-      if (!pubw) load_p2(l, tid);
       red_put(s, w, lane, acc);
+      if (!pubw) load_p2(l, tid);
       __syncthreads();
       CE_SUB(2);
       if (pubw) {
@@ -344,6 +374,13 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       const int grp = lane / LPK, sub = lane % LPK;
       const int vsel = min(grp, NREP + 1);
       const int e0 = sub * 8, half = D / 2, ec = e0 % half;
+      // the norm weights and rotary rows do not depend on the edge: issued before its wait
+      float nwv[8], cv[8], sv[8];
+      const float* qn = (const float*)lp(PT_QN, l);
+      const float* kn = (const float*)lp(PT_KN, l);
+      load8f((vsel < NREP ? qn : kn) + e0, nwv);
+      load8f(p.cos_tab + (long long)kvpos * half + ec, cv);
+      load8f(p.sin_tab + (long long)kvpos * half + ec, sv);
       float xv[8];
       if (l == 0) {
         const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
@@ -356,10 +393,6 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
       }
       CE_STAMP(sb + 3);
-      float nwv[8], cv[8], sv[8];
-      load8f((vsel < NREP ? p.q_norm[l] : p.k_norm[l]) + e0, nwv);
-      load8f(p.cos_tab + (long long)kvpos * half + ec, cv);
-      load8f(p.sin_tab + (long long)kvpos * half + ec, sv);
       {  // q/k RMSNorm + RoPE (branch-free over the lane groups; the v group's result is discarded)
         const bool lo = e0 < half, normed = vsel <= NREP;
         float ss = 0.f;
@@ -464,21 +497,22 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments 2w, 2w + 1 of tile 2cg + w / 4
       {
         const int kt0 = (2 * w) % 8;
+        u32x4_t af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = *(const u32x4_t*)(lm < NW ? &s.att[lm][(kt0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
+        asm volatile("" : "+v"(af[0]), "+v"(af[1]));
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const u32x4_t av = lm < NW ? *(const u32x4_t*)&s.att[lm][(kt0 + i) * 32 + lk * 8] : u32x4_t{0u, 0u, 0u, 0u};
-          acc = mfma(av, w2[i], acc);
-        }
+        for (int i = 0; i < 2; ++i) acc = mfma(af[i], w2[i], acc);
         CE_AFTER(acc);
-        if (!pubw) load_p3(l, tid);
         red_put(s, w, lane, acc);
+        if (!pubw) load_p3(l, tid);
         // the new k / v of (row w, head h) into the caches (one column group appends)
         if (cg == 0 && w < R && lane < D / 2) {
           const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
-          ((unsigned*)p.k_cache[l])[o / 2 + lane] = s.kn2[w][lane];
-          ((bf16_t*)p.v_cache[l])[o + lane] = f2bf(s.vn[w][lane]);
-          ((bf16_t*)p.v_cache[l])[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
+          ((unsigned*)lp(PT_KC, l))[o / 2 + lane] = s.kn2[w][lane];
+          ((bf16_t*)lp(PT_VC, l))[o + lane] = f2bf(s.vn[w][lane]);
+          ((bf16_t*)lp(PT_VC, l))[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
         }
       }
       __syncthreads();
@@ -535,14 +569,19 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
                 err, tid);
       CE_STAMP(sb + 8);
       const int k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4, n3 = ntile3 == 2 ? 8 : 4;
+      u32x4_t af[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = afrag_x(s, lm, lk, k3 + min(i, n3 - 1), R);
+      pin4(af);
+      pin4(af + 4);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        if (i < n3) acc = mfma(afrag_x(s, lm, lk, k3 + i, R), w3[i], acc);
+        if (i < n3) acc = mfma(af[i], w3[i], acc);
       CE_AFTER(acc);
       CE_SUB(12);
-      if (!pubw) load_p4(l, tid);
       red_put(s, w, lane, acc);
+      if (!pubw) load_p4(l, tid);
       __syncthreads();
       CE_SUB(14);
       if (pubw) {  // SwiGLU of (tile j, row rr, column pair pp) from the partials, every replica, drain, flags
@@ -597,18 +636,23 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       CE_SUB(22);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const int kt = w * 12 + i;
-        const u32x4_t av = lm < 2 ? *(const u32x4_t*)&s.a.ha[lm][kt * 32 + lk * 8] : u32x4_t{0u, 0u, 0u, 0u};
-        acc = mfma(av, w4[i], acc);
+      for (int i0 = 0; i0 < 12; i0 += 6) {
+        u32x4_t af[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+          af[i] = *(const u32x4_t*)(lm < 2 ? &s.a.ha[lm][(w * 12 + i0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
+        pin4(af);
+        asm volatile("" : "+v"(af[4]), "+v"(af[5]));
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc = mfma(af[i], w4[i0 + i], acc);
       }
       CE_AFTER(acc);
       auto next_w1 = [&]() {
-        if (l + 1 < L) load_p1(p.w_qkv[l + 1], (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, tid);
+        if (l + 1 < L) load_p1(lp(PT_QKV, l + 1), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, tid);
         else if (b < p.V / 16) load_p1(p.w_lm, (unsigned)p.V * H * 2, b, tid);
       };
-      if (!pubw) next_w1();
       red_put(s, w, lane, acc);
+      if (!pubw) next_w1();
       __syncthreads();
       CE_SUB(25);
       if (pubw) {
