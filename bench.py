@@ -121,7 +121,7 @@ def _gemv_entry(name, kernel, n_frame, Ws, M, K, N, a_dtype, o_dtype, dev, rms=F
     return dict(name=name, kernel=kernel, bound="hbm", launches_per_frame=n_frame, avg_us=us, bytes=byt)
 
 
-def attn_oproj_entry(tts, B, pos=9, reps=20):
+def attn_oproj_entry(tts, B, pos=9, reps=20, n_frame=None):
     """Code-predictor fused attention + o_proj + residual (attn_oproj_k) at cache position `pos` (the mean over the 14
     decode steps), 5 launches over the 5 layers' distinct o_proj weights per replay.  Algorithmic bytes per launch =
     o_proj weights + K/V of (pos + 1) keys + the q/k/v rows read + the residual read and written (fp32 + bf16)."""
@@ -147,8 +147,39 @@ def attn_oproj_entry(tts, B, pos=9, reps=20):
            + B * c.qkv_w * 4 + B * c.H * (4 + 4 + (2 if x16 is not None else 0)))
     kname = "attn_oproj_hs_k (head-split" if ws is not None else "attn_oproj_k ("
     return dict(name="cp_attn_oproj", kernel=f"{kname} code-predictor attention + o_proj + residual, {pos + 1} keys)",
-                bound="hbm", launches_per_frame=5 * (eng.G - 2), avg_us=us, bytes=byt,
+                bound="hbm", launches_per_frame=5 * (eng.G - 2) if n_frame is None else n_frame, avg_us=us, bytes=byt,
                 pmc_tag="attn_oproj_hs" if ws is not None else "attn_oproj")
+
+
+def cp_step_entry(tts, B, Lmax=18, reps=20):
+    """The code-predictor step engine (cp_step_k: 5 layers + lm_head[g] in one persistent launch), the 14 decode steps
+    of a frame (cache positions 2..15, lm_head 1..14) captured in one graph.  Algorithmic bytes per launch = the 5
+    layers' weights + lm_head[g] + the K/V rows read (pos keys per layer) and the new key written + x, the layer-0
+    q/k/v rows and the logits."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    c, dev = eng.cp, eng.dev
+    kc = [torch.randn(B, c.Hkv, Lmax, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    vc = [torch.randn(B, c.Hkv, Lmax, c.D, device=dev).to(eng.kv_dtype) for _ in c.layers]
+    qkv = torch.randn(B, c.qkv_w, device=dev)
+    x = torch.randn(B, c.H, device=dev)
+    logits = torch.empty(B, eng.Vc, device=dev)
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+    steps = list(range(1, eng.G - 1))
+
+    def run():
+        for g in steps:
+            Kn.cp_step(c.layers, eng.lm_heads[g], x, qkv, B, kc, vc, Lmax, g + 1, c.cos, c.sin, c.eps, logits, ws)
+    us = _graph_us(run, dev, reps) / len(steps)
+    assert int(ws[:4].view(torch.int32).item()) == 0, "cp_step hand-off flag set during the kernel-table run"
+    L0 = c.layers[0]
+    wb = sum(W.w.numel() * W.w.element_size() for W in (L0.qkv, L0.o, L0.gu, L0.down)) * len(c.layers)
+    lm = eng.lm_heads[1].w.numel() * eng.lm_heads[1].w.element_size()
+    el = kc[0].element_size()
+    kv = sum(len(c.layers) * B * c.Hkv * c.D * el * (2 * (g + 1) + 2) for g in steps) / len(steps)
+    byt = int(wb + lm + kv + B * (c.H + c.qkv_w + eng.Vc) * 4)
+    return dict(name="cp_step", kernel="cp_step_k (code-predictor step engine: 5 layers + lm_head in one launch, "
+                "keys 2..15)", bound="hbm", launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
 
 
 def decode_kernel_table(tts, B, L_mean):
@@ -162,6 +193,9 @@ def decode_kernel_table(tts, B, L_mean):
     bf = torch.bfloat16
     G = eng.G
     n_cp = G - 1  # CP forwards per frame: the 2-token prefill + 14 decode steps
+    # with the step engine (qt_cp_step) the 14 decode steps are one launch each; the launch chain runs the prefill only
+    engine = any(s.cp.ce_ws is not None for s in eng.all_sessions())
+    n_dec = 0 if engine else n_cp - 1  # decode-step forwards on the launch chain
     tab = [
         _gemv_entry("talker_gateup", "gemv_wt (talker MLP gate/up + SwiGLU, RMS folded)", t.n_layers,
                     [L.gu for L in t.layers], B, t.H, 2 * t.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
@@ -171,17 +205,20 @@ def decode_kernel_table(tts, B, L_mean):
                     t.qkv_w, bf, torch.float32, dev, rms=True),
         _gemv_entry("talker_o", "gemv_wt (talker o_proj + residual)", t.n_layers, [L.o for L in t.layers], B,
                     t.Hq * t.D, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
-        _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * n_cp,
+        _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * (1 + n_dec),
                     [L.gu for L in c.layers], B, c.H, 2 * c.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
-        _gemv_entry("cp_down", "gemv_wt (code-predictor down + residual)", c.n_layers * n_cp, [L.down for L in c.layers],
+        _gemv_entry("cp_down", "gemv_wt (code-predictor down + residual)", c.n_layers * (1 + n_dec),
+                    [L.down for L in c.layers],
                     B, c.I, c.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
         _gemv_entry("cp_qkv", "gemv_wt (code-predictor q/k/v, layers 1-4 of decode steps + prefill)",
-                    (c.n_layers - 1) * (n_cp - 1) + c.n_layers, [L.qkv for L in c.layers], B, c.H, c.qkv_w, bf,
+                    (c.n_layers - 1) * n_dec + c.n_layers, [L.qkv for L in c.layers], B, c.H, c.qkv_w, bf,
                     torch.float32, dev, rms=True),
-        _gemv_entry("cp_lm_head", "gemv_wt (code-predictor lm_head, final norm folded)", n_cp, eng.lm_heads, B, c.H,
+        _gemv_entry("cp_lm_head", "gemv_wt (code-predictor lm_head, final norm folded)", 1 + n_dec, eng.lm_heads, B, c.H,
                     eng.Vc, bf, torch.float32, dev, rms=True),
-        attn_oproj_entry(tts, B),
+        attn_oproj_entry(tts, B, n_frame=c.n_layers * (1 + n_dec)),
     ]
+    if engine:
+        tab.append(cp_step_entry(tts, B))
     ra = attention_roofline(tts, B, L_mean)
     tab.append(dict(name="talker_attention", kernel=f"attn_decode_k (talker decode attention, {L_mean} keys)",
                     bound="hbm", launches_per_frame=t.n_layers, avg_us=ra["avg_us"], bytes=ra["bytes"]))
@@ -210,7 +247,7 @@ def _pmc_traffic(tag):
     return None, None
 
 
-PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj"}
+PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj", "cp_step": "cp_step"}
 
 
 def _rocprof_avg(tag):
