@@ -209,7 +209,16 @@ QT_DEV void red_put(Lds& s, int w, int lane, f32x4_t acc) {
   s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
 }
 
+// When the next phase's weight fragments are issued (LM):
+//  0 (early): by waves 1-7 right after their MFMAs, by the publishing wave after its flag -- the other waves' ~100 KiB
+//    of loads then sit in the CU's memory pipeline ahead of the publisher's stores, drain and flag (critical path);
+//  1 (late): by every wave after the phase's publication (one more block barrier) -- but a wave's edge poll / payload
+//    loads then return behind its own weight loads (vmcnt is in order), so every edge also waits one weight round trip;
+//  2 (ahead): one phase ahead, right after the edge that starts the previous phase (before its MFMAs): the memory
+//    pipeline has drained them by the time that phase publishes, and they have landed before the next edge's polls.
+template <int LM>
 __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
+  constexpr bool LATE = LM == 1, AHEAD = LM == 2, EARLY = LM == 0;
   const qt_cp_step_args& p = pk.a;
   __shared__ Lds s;
   const int b = blockIdx.x, h = b >> 5, cg = b & 31;
@@ -338,6 +347,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
                 tagof(5 * (l - 1) + 4), R, p.eps, pk.spin, err, tid);
       CE_STAMP(sb + 1);
+      if (AHEAD) load_p2(l, tid);
       u32x4_t af[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = afrag_x(s, lm, lk, w * 4 + i, R);
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       CE_AFTER(acc);
       CE_SUB(0);
       red_put(s, w, lane, acc);
-      if (!pubw) load_p2(l, tid);
+      if (EARLY && !pubw) load_p2(l, tid);
       __syncthreads();
       CE_SUB(2);
       if (pubw) {
@@ -364,6 +374,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         drain_stores();
         CE_SUB(4);
         if (lane == 0) st_flag(flags + b, tagof(5 * l));
+        if (EARLY) load_p2(l, tid);
+      }
+      if (LATE) {
+        __syncthreads();
         load_p2(l, tid);
       }
       CE_STAMP(sb + 2);
@@ -492,6 +506,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       }
       __syncthreads();
       CE_STAMP(sb + 4);
+      if (AHEAD) load_p3(l, tid);
       if (dbg && l == 0 && cg == 0 && w < R)
         for (int j = lane; j < NREP * D; j += 64) dbg[((size_t)3 * MAXR + w) * 4096 + h * NREP * D + j] = bf2f(s.att[w][j]);
       // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments 2w, 2w + 1 of tile 2cg + w / 4
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         for (int i = 0; i < 2; ++i) acc = mfma(af[i], w2[i], acc);
         CE_AFTER(acc);
         red_put(s, w, lane, acc);
-        if (!pubw) load_p3(l, tid);
+        if (EARLY && !pubw) load_p3(l, tid);
         // the new k / v of (row w, head h) into the caches (one column group appends)
         if (cg == 0 && w < R && lane < D / 2) {
           const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
@@ -559,6 +574,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
             dbg[((size_t)0 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
         }
         publish_x16(0, tagof(5 * l + 2), lane);  // (the wave's own LDS writes above are complete: one wave, in order)
+        if (EARLY) load_p3(l, tid);
+      }
+      if (LATE) {
+        __syncthreads();
         load_p3(l, tid);
       }
       CE_STAMP(sb + 7);
@@ -568,6 +587,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16), fl_off(myrep, FL_X0), tagof(5 * l + 2), R, p.eps, pk.spin,
                 err, tid);
       CE_STAMP(sb + 8);
+      if (AHEAD) load_p4(l, tid);
       const int k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4, n3 = ntile3 == 2 ? 8 : 4;
       u32x4_t af[8];
 #pragma unroll
@@ -581,7 +601,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       CE_AFTER(acc);
       CE_SUB(12);
       red_put(s, w, lane, acc);
-      if (!pubw) load_p4(l, tid);
+      if (EARLY && !pubw) load_p4(l, tid);
       __syncthreads();
       CE_SUB(14);
       if (pubw) {  // SwiGLU of (tile j, row rr, column pair pp) from the partials, every replica, drain, flags
@@ -610,6 +630,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         drain_stores();
         CE_SUB(18);
         if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, FL_H)) + b, tagof(5 * l + 3));
+        if (EARLY) load_p4(l, tid);
+      }
+      if (LATE) {
+        __syncthreads();
         load_p4(l, tid);
       }
       CE_STAMP(sb + 9);
@@ -634,6 +658,11 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       CE_SUB(21);
       __syncthreads();
       CE_SUB(22);
+      auto next_w1 = [&]() {
+        if (l + 1 < L) load_p1(lp(PT_QKV, l + 1), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, tid);
+        else if (b < p.V / 16) load_p1(p.w_lm, (unsigned)p.V * H * 2, b, tid);
+      };
+      if (AHEAD) next_w1();
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i0 = 0; i0 < 12; i0 += 6) {
@@ -647,12 +676,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         for (int i = 0; i < 6; ++i) acc = mfma(af[i], w4[i0 + i], acc);
       }
       CE_AFTER(acc);
-      auto next_w1 = [&]() {
-        if (l + 1 < L) load_p1(lp(PT_QKV, l + 1), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, tid);
-        else if (b < p.V / 16) load_p1(p.w_lm, (unsigned)p.V * H * 2, b, tid);
-      };
       red_put(s, w, lane, acc);
-      if (!pubw) next_w1();
+      if (EARLY && !pubw) next_w1();
       __syncthreads();
       CE_SUB(25);
       if (pubw) {
@@ -665,6 +690,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
             dbg[((size_t)2 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
         }
         publish_x16(1, tagof(5 * l + 4), lane);
+        if (EARLY) next_w1();
+      }
+      if (LATE) {
+        __syncthreads();
         next_w1();
       }
       CE_STAMP(sb + 11);
@@ -703,10 +732,13 @@ bool cp_step_resident() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
   if (cap[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cp_step_k, NT, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
+    int per_cu = 1 << 20, cus = 0;  // every load-timing variant
+    for (const void* k : {(const void*)cp_step_k<0>, (const void*)cp_step_k<1>, (const void*)cp_step_k<2>}) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, NT, 0) != hipSuccess) return false;
+      per_cu = std::min(per_cu, n);
+    }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
     cap[dev] = std::max(1, per_cu * cus);
   }
   return cap[dev] >= NB;
@@ -736,6 +768,10 @@ extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
       return QT_ERR_ARG;
   if (!cp_step_resident()) return QT_ERR_SHAPE;
   static const int spin = std::max(1000, qt_knob("QT_CE_SPIN", 200000));
-  hipLaunchKernelGGL(cp_step_k, dim3(NB), dim3(NT), 0, (hipStream_t)stream, CEP{*a, spin});
+  static const int lm = qt_knob("QT_CE_LM", 1);  // load timing (probe builds only: the product reads no env)
+  const CEP pk{*a, spin};
+  if (lm == 0) hipLaunchKernelGGL(cp_step_k<0>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else if (lm == 1) hipLaunchKernelGGL(cp_step_k<1>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else hipLaunchKernelGGL(cp_step_k<2>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }

@@ -110,9 +110,10 @@ _LIB = None
 BUILD_ID = None  # qt_build_id() of the loaded library (digest of the sources it was built from)
 
 
-def source_digest():
-    """Digest of the kernel sources shipped next to this package (qwen3-tts_amd/build.py's source_digest), or
-    None when they are absent (an installed copy without sources)."""
+def source_digest(probe=False):
+    """Digest of the kernel sources shipped next to this package (qwen3-tts_amd/build.py's source_digest; the probe
+    build's carries its flags and a "-probe" suffix), or None when they are absent (an installed copy without
+    sources)."""
     bpath = os.path.join(os.path.dirname(HERE), "build.py")
     if not os.path.exists(bpath) or not os.path.isdir(os.path.join(os.path.dirname(HERE), "csrc")):
         return None
@@ -120,7 +121,7 @@ def source_digest():
     spec = importlib.util.spec_from_file_location("_qt_build", bpath)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    return mod.source_digest()
+    return mod.source_digest(probe=probe) + ("-probe" if probe else "")
 
 
 def load_library(path: str = LIB_PATH):
@@ -134,7 +135,7 @@ def load_library(path: str = LIB_PATH):
     L.qt_build_id.restype = ctypes.c_char_p
     L.qt_build_id.argtypes = []
     bid = L.qt_build_id().decode()
-    want = source_digest() if path == LIB_PATH else None
+    want = source_digest(probe=os.path.basename(path).endswith("_probe.so")) if path == LIB_PATH else None
     if want is not None and bid != want and os.environ.get("QT_ALLOW_STALE_LIB") != "1":
         raise RuntimeError(f"{path} was built from other sources (build id {bid}, sources {want}): rebuild with "
                            "`python qwen3-tts_amd/build.py`")
