@@ -43,7 +43,7 @@ def main():
     st.n_layers = len(all_layers)
 
 
-if __name__ == "__main__" and not os.environ.get("CE_LAYER0"):
+if __name__ == "__main__" and not (os.environ.get("CE_LAYER0") or os.environ.get("CE_STAMPS") or os.environ.get("CE_TIME")):
     main()
 
 
@@ -138,3 +138,38 @@ def stamps(R=8, reps=3):
 
 if __name__ == "__main__" and os.environ.get("CE_STAMPS"):
     stamps()
+
+
+def timing(R=8, reps=50):
+    """Device time per launch of 14 consecutive engine launches (cache positions 2..15) captured in one HIP graph,
+    HIP events on the capture stream (no stamps: the product library)."""
+    dev = torch.device("cuda:0")
+    st, lm, g = _cp_stack(dev)
+    Lmax = 18
+    x, x16, qkv0, kc, vc = _inputs(st, R, Lmax, g, dev)
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+    logits = torch.empty(R, lm.N, device=dev)
+
+    def run():
+        for pos in range(2, 16):
+            Kn.cp_step(st.layers, lm, x, qkv0, R, kc, vc, Lmax, pos, st.cos, st.sin, st.eps, logits, ws)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            run()
+        gr.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            gr.replay()
+        e1.record(s)
+    torch.cuda.synchronize()
+    print(f"graph of 14 launches x {reps}: {e0.elapsed_time(e1) * 1e3 / (14 * reps):.2f} us per launch, "
+          f"error flag {int(ws[:4].view(torch.int32).item())}")
+
+
+if __name__ == "__main__" and os.environ.get("CE_TIME"):
+    timing()
