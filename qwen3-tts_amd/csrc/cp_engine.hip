@@ -28,12 +28,12 @@
 // attn_oproj_hs_k (q and keys as bf16 pairs, fp32 softmax), SwiGLU / attention outputs rounded to bf16.
 #include "common.h"
 #include "attn_dev.h"
+#include "engine_dev.h"
 #include <algorithm>
 
 namespace {
 
-typedef unsigned long long u64;
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
+using namespace qt_engine;
 
 constexpr int H = 1024, I = 3072, D = 128, NQ = 16, NKV = 8, NREP = 2;
 constexpr int NB = 256, NW = 8, NT = NW * 64, MAXR = 8;
@@ -70,50 +70,6 @@ struct CEP {
   qt_cp_step_args a;
   int spin;
 };
-
-// ---- memory primitives
-QT_DEV rsrc_t mkr(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-constexpr int SC1 = 16;  // buffer-instruction cache policy: sc1 (agent-coherent, write-through)
-QT_DEV u32x4_t bld(rsrc_t r, unsigned off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0); }
-QT_DEV u32x4_t bld_c(rsrc_t r, unsigned off) { return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SC1); }
-QT_DEV uint2 bld2_c(rsrc_t r, unsigned off) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SC1);
-  return uint2{v[0], v[1]};
-}
-QT_DEV void bst_c(unsigned v, rsrc_t r, unsigned off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, SC1); }
-QT_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-QT_DEV unsigned ld_flag(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-QT_DEV void st_flag(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-QT_DEV u64 ld_g(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-QT_DEV void st_g(u64* p, unsigned v, unsigned tag) {
-  __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-QT_DEV f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0,
-                                                 0, 0);
-}
-// byte offset of lane `lane`'s 16 bytes of weight fragment (n tile, k tile) of a pre-tiled bf16 matrix with kt k tiles
-QT_DEV unsigned fragoff(int nt, int ktile, int kt, int lane) { return ((unsigned)(nt * kt + ktile) << 10) + lane * 16; }
-// keep issued loads where they are (not sunk to their first use)
-#define CE_ISSUED() asm volatile("" ::: "memory")
-// LDS-DMA (global_load_lds_dwordx4, no VGPR staging): lane l's 16 bytes land at lds + 16 l; hipcc does not count it,
-// the issuing wave waits with its own s_waitcnt vmcnt before reading (vmcnt is in order, so every compiler wait on a
-// later load also covers it)
-QT_DEV void glds16(const void* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-QT_DEV unsigned lds_u32(const void* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
-}
-QT_DEV void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// the phase's MFMAs are issued before the next phase's weight loads (so the two weight sets are never live together)
-// all four A fragments read (one LDS wait) before the first MFMA, instead of a wait per MFMA
-QT_DEV void pin4(u32x4_t* a) { asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3])); }
-#define CE_AFTER(acc) asm volatile("" : "+v"(acc)::"memory")
 
 // Wave 0 (the publishing wave) waits until the n (multiple of 4, <= 256) flag words at byte offset `off` all carry
 // `tag` -- one 16-byte sc1 load per lane per pass -- (bounded: a give-up sets the sticky error flag), then a block

@@ -1,0 +1,494 @@
+// Talker decode-layer tail engine for gfx950: ONE persistent launch runs the part of a talker decoder layer after its
+// attention -- o_proj + residual -> post-attention RMSNorm + gate/up + SwiGLU -> down + residual -> the NEXT layer's
+// input RMSNorm + q/k/v projection -- for up to 8 batch rows, where the launch chain issued four weight-streaming
+// GEMV kernels.  Replaces M:961-1012 after the attention call (o_proj M:804, residual M:991, MLP
+// M:995-1004 with Qwen3TTSTalkerTextMLP / the talker's SwiGLU) and the next layer's input_layernorm + q/k/v
+// projections (M:985, M:752-754) of Qwen3TTSTalkerModel.forward's decode step (M:1430-1480).
+//
+// Why one launch: the four GEMVs stream 101 MB of bf16 weights per layer (1.7B talker); as separate launches each pays
+// a launch ramp and tail (3.3 TB/s over the four, `profiles/r05_bench_line.json` kernel table).  Here the weights
+// stream continuously: two LOADER waves per workgroup move the block's weight fragments, in the order the block
+// consumes them, into an LDS ring by LDS-DMA (global_load_lds, non-temporal: read once per frame), running ahead of
+// the eight CONSUMER waves by up to the ring's depth -- so the weights of the next phase arrive while the consumers
+// wait for a hand-off -- and the consumers, whose own loads are only the hand-off polls and payloads, never wait
+// behind a weight round trip (vmcnt retires in order per wave).
+//
+// Geometry: 256 workgroups (one per CU, all resident -- the host checks the occupancy) x (8 consumer + 2 loader)
+// waves.  Block b:  o_proj and down: output tile t = b / 2 (16 of 2048 columns), K half b % 2 (split-K pair; the even
+// block OWNS x[rows][16t .. 16t + 16) and receives the odd block's partial as 8-byte {value, tag} granules);
+// gate/up: tiles b, b + 256, b + 512 (768 tiles of 8 gate + 8 up columns); next q/k/v: tile b (256 tiles).
+// Hand-offs: x16 after each residual (all-to-all) and the SwiGLU rows (all-to-all) in the R1 form with one replica
+// per XCD (as qt_cp_step), the split-K pairs as granules.  Tags: epoch * 8 + edge + 1, the epoch a launch counter in
+// the workspace advanced by block 0 at the end.
+#include "common.h"
+#include "engine_dev.h"
+#include <algorithm>
+
+namespace {
+
+using namespace qt_engine;
+
+constexpr int H = 2048, I = 6144, NQKV = 4096, KO = 2048;  // the 1.7B talker
+constexpr int NB = 256, NWC = 8, NWL = 2, NT = (NWC + NWL) * 64, MAXR = 8;
+constexpr int KTH = H / 32, KTI = I / 32, KTO = KO / 32;  // 64 / 192 / 64 k tiles
+constexpr int NSLOT = 5, SLOT = 16;                       // ring: 5 slots x 16 fragments (16 KiB)
+constexpr int XLD = H + 8, ALD = KO / 2 + 8, HLD = I / 2 + 8;
+constexpr int NEDGE = 8;
+constexpr int NPRE = 8;  // ring slots a consumer wave holds in registers across a hand-off wait
+constexpr int E_PO = 0, E_X1 = 1, E_H = 2, E_PD = 3, E_X2 = 4;
+// slots per phase: o_proj 32 k tiles, gate/up 3 tiles x 64, down 96 k tiles, q/k/v 64
+constexpr int S_O = KTO / 2 / SLOT, S_GU = 3 * KTH / SLOT, S_D = KTI / 2 / SLOT, S_Q = KTH / SLOT;
+static_assert(S_O == 2 && S_GU == 12 && S_D == 6 && S_Q == 4, "slot plan");
+
+// workspace (bytes)
+constexpr size_t OFF_ERR = 0, OFF_EPOCH = 4;
+constexpr int NREPL = 8;
+constexpr int FL_X1 = 0, FL_H = 1, FL_X2 = 2;
+constexpr size_t OFF_FLAGS = 256, REPL_FLAGS = (size_t)3 * NB * 4;
+constexpr size_t OFF_PART = OFF_FLAGS + NREPL * REPL_FLAGS;             // [2][128 tiles][MAXR][16] granules
+constexpr size_t OFF_X16 = OFF_PART + (size_t)2 * 128 * MAXR * 16 * 8;
+constexpr size_t REPL_X16 = (size_t)2 * MAXR * (H / 2) * 4;            // [2 bufs][MAXR][H/2] bf16 pairs
+constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;
+constexpr size_t REPL_H = (size_t)MAXR * (I / 2) * 4;                  // [MAXR][I/2] bf16 pairs
+constexpr size_t WS_BYTES = OFF_H + NREPL * REPL_H;
+constexpr size_t STAMP_BYTES = (size_t)NB * 32 * 8;                    // optional per-block phase stamps
+
+struct TP {
+  qt_talker_tail_args a;
+  int spin;
+};
+
+struct TLds {
+  __attribute__((aligned(16))) unsigned char ring[NSLOT][SLOT * 1024];
+  union {
+    bf16_t xa[MAXR][XLD];  // x16 rows: the A operand of gate/up and q/k/v
+    bf16_t aa[MAXR][ALD];  // the attention rows' K half: the A operand of o_proj
+    bf16_t ha[MAXR][HLD];  // the SwiGLU rows' K half: the A operand of down
+  } a;
+  float red[2][NWC][64][4];                     // per-wave MFMA partials (double-buffered: gate/up tiles)
+  float rs[MAXR];                               // 1 / rms per row
+  float xo[MAXR][16];                           // owner: the residual slice (fp32)
+  unsigned hb[3][MAXR][4];                      // this block's SwiGLU output pairs
+  __attribute__((aligned(16))) bf16_t zero[32];
+  unsigned full[NSLOT];                         // ring slot s % NSLOT holds sequence number s (+1)
+  unsigned done[NWC];                           // consumer wave w has finished with sequences < done[w]
+};
+
+QT_DEV void glds16_nt(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+QT_DEV unsigned lds_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+QT_DEV void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// The consumer waves synchronise among themselves only: the loader waves run free, so a block-wide s_barrier cannot
+// be used once they have split off.  The consumers meet through an LDS arrival counter instead (generation-counted,
+// bounded spin: a give-up sets error bit 8).
+
+struct CBar {
+  unsigned* cnt;  // LDS: arrivals
+  unsigned* gen;  // LDS: generation
+};
+QT_DEV void cons_sync(const CBar& cb, unsigned& g, int spin, int* err) {
+  // every consumer wave's LDS writes before the barrier are visible after it: the wave's own LDS operations complete
+  // (lgkmcnt(0)) before its arrival, an LDS atomic
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int lane = threadIdx.x & 63;
+  ++g;
+  if (lane == 0) {
+    const unsigned a = __hip_atomic_fetch_add(cb.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (a == g * NWC - 1) lds_st(cb.gen, g);
+  }
+  for (int spins = 0; __builtin_amdgcn_readfirstlane(lds_ld(cb.gen)) < g; ++spins) {
+    if (spins > 64 * spin) { if (lane == 0) atomicOr(err, 8); break; }
+    __builtin_amdgcn_s_sleep(0);
+  }
+}
+
+__global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
+  const qt_talker_tail_args& p = pk.a;
+  __shared__ TLds s;
+  __shared__ unsigned cb_cnt, cb_gen;
+  const int b = blockIdx.x;
+  const int ot = b >> 1, kh = b & 1;  // o_proj / down: tile, K half
+  const bool owner = kh == 0;
+  const int R = p.R;
+  const bool has_next = p.w_qkv_next != nullptr;
+  char* ws = (char*)p.ws;
+  int* err = (int*)(ws + OFF_ERR);
+  const int myrep = b % NREPL;
+  auto fl_off = [&](int rp, int kind) { return (unsigned)(OFF_FLAGS + rp * REPL_FLAGS + kind * NB * 4); };
+  u64* gpart = (u64*)(ws + OFF_PART);
+  const rsrc_t wsr = mkr(ws, (unsigned)WS_BYTES);
+  const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);
+  auto tagof = [&](int e) { return ep * NEDGE + (unsigned)e + 1u; };
+  u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES) + b * 32 : nullptr;
+#define TT_STAMP(k) \
+  if (kProbe && stamps && threadIdx.x == 0) stamps[(k)] = __builtin_amdgcn_s_memrealtime();
+  TT_STAMP(0);
+  const int nseq = S_O + S_GU + S_D + (has_next ? S_Q : 0);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+
+  if (tid < NSLOT) s.full[tid] = 0u;
+  else if (tid >= 64 && tid < 64 + NWC) s.done[tid - 64] = 0u;
+  else if (tid >= 128 && tid < 144) ((unsigned*)s.zero)[tid - 128] = 0u;
+  if (tid == 0) { cb_cnt = 0u; cb_gen = 0u; }
+  __syncthreads();  // (the last block-wide barrier: the loader waves run free from here)
+
+  if (w >= NWC) {
+    // ------------------------------------------------------------------ loader waves
+    const int lw = w - NWC;
+    for (int sq = lw; sq < nseq; sq += NWL) {
+      const void* W;
+      int tile, kt0, KT;
+      if (sq < S_O) { W = p.w_o; tile = ot; kt0 = kh * (KTO / 2) + SLOT * sq; KT = KTO; }
+      else if (sq < S_O + S_GU) { const int j = sq - S_O; W = p.w_gu; tile = b + NB * (j / 4); kt0 = SLOT * (j % 4); KT = KTH; }
+      else if (sq < S_O + S_GU + S_D) { const int j = sq - S_O - S_GU; W = p.w_down; tile = ot; kt0 = kh * (KTI / 2) + SLOT * j; KT = KTI; }
+      else { const int j = sq - S_O - S_GU - S_D; W = p.w_qkv_next; tile = b; kt0 = SLOT * j; KT = KTH; }
+      const int slot = sq % NSLOT;
+      if (sq >= NSLOT) {  // the slot's previous sequence consumed by every consumer wave
+        for (int spins = 0;; ++spins) {
+          unsigned m = 0xFFFFFFFFu;
+#pragma unroll
+          for (int c = 0; c < NWC; ++c) m = min(m, lds_ld(&s.done[c]));
+          if ((int)__builtin_amdgcn_readfirstlane(m) >= sq - NSLOT + 1) break;
+          if (spins > pk.spin) { if (lane == 0) atomicOr(err, 2); break; }
+          __builtin_amdgcn_s_sleep(0);
+        }
+      }
+      const char* src = (const char*)W + ((size_t)(tile * KT + kt0) << 10) + lane * 16;
+      const unsigned dst = lds_u32(&s.ring[slot][0]);
+#pragma unroll
+      for (int f = 0; f < SLOT; ++f) glds16_nt(src + f * 1024, dst + f * 1024);
+      // this wave's previous slot has landed once only this slot's 16 transfers are outstanding
+      if (sq - NWL >= 0) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if (lane == 0) lds_st(&s.full[(sq - NWL) % NSLOT], (unsigned)(sq - NWL + 1));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int last = lw + NWL * ((nseq - 1 - lw) / NWL);  // this wave's last sequence
+    if (lane == 0 && last < nseq) lds_st(&s.full[last % NSLOT], (unsigned)(last + 1));
+    return;
+  }
+
+  // ------------------------------------------------------------------ consumer waves (tid < 512)
+  CBar cb{&cb_cnt, &cb_gen};
+  unsigned cg = 0;  // consumer barrier generation
+  const int lm = lane & 15, lk = lane >> 4;
+  int sq = 0;  // next ring sequence
+  // one ring slot: wait until it is full, read this wave's two fragments, release it
+  auto take = [&](u32x4_t& f0, u32x4_t& f1) {
+    const int slot = sq % NSLOT;
+    for (int spins = 0; (int)__builtin_amdgcn_readfirstlane(lds_ld(&s.full[slot])) < sq + 1; ++spins) {
+      if (spins > pk.spin) { if (lane == 0) atomicOr(err, 4); break; }
+      __builtin_amdgcn_s_sleep(0);
+    }
+    f0 = *(const u32x4_t*)&s.ring[slot][(2 * w) * 1024 + lane * 16];
+    f1 = *(const u32x4_t*)&s.ring[slot][(2 * w + 1) * 1024 + lane * 16];
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1)::"memory");
+    ++sq;
+    if (lane == 0) lds_st(&s.done[w], (unsigned)sq);
+  };
+  // Before each hand-off wait every consumer wave copies its fragments of the next phase's first n ring slots into
+  // registers and releases the slots: the ring (5 LDS slots, ~3 us of stream) would otherwise fill during the wait
+  // and stall the loaders; registers extend it by NPRE slots.
+  u32x4_t pf[2 * NPRE];
+  auto pretake = [&](int n) {
+#pragma unroll
+    for (int k = 0; k < NPRE; ++k)
+      if (k < n) take(pf[2 * k], pf[2 * k + 1]);
+  };
+  auto frags = [&](int k, u32x4_t& f0, u32x4_t& f1) {  // slot k of the phase: pre-taken or from the ring
+    if (k < NPRE) { f0 = pf[2 * k]; f1 = pf[2 * k + 1]; } else take(f0, f1);
+  };
+  auto wait_flags = [&](unsigned off, int n, unsigned tag) {
+    if (w == 0) {
+      for (int spins = 0;; ++spins) {
+        bool ok = true;
+        if (lane * 4 < n) {
+          const u32x4_t v = bld_c(wsr, off + lane * 16);
+          ok = v[0] == tag && v[1] == tag && v[2] == tag && v[3] == tag;
+        }
+        if (__all(ok)) break;
+        if (spins > pk.spin) { if (lane == 0) atomicOr(err, 1); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    cons_sync(cb, cg, pk.spin, err);
+  };
+  auto red_put = [&](int buf, f32x4_t acc) {
+    s.red[buf][w][lane][0] = acc[0]; s.red[buf][w][lane][1] = acc[1];
+    s.red[buf][w][lane][2] = acc[2]; s.red[buf][w][lane][3] = acc[3];
+  };
+  auto red_sum = [&](int buf) {  // (wave 0) the 8 waves' partials of MFMA lane `lane`, in wave order
+    f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ww = 0; ww < NWC; ++ww) {
+      v[0] += s.red[buf][ww][lane][0]; v[1] += s.red[buf][ww][lane][1];
+      v[2] += s.red[buf][ww][lane][2]; v[3] += s.red[buf][ww][lane][3];
+    }
+    return v;
+  };
+  // x16 rows from replica myrep of buffer `buf` -> s.a.xa, 1 / rms per row: thread -> row tid / 64
+  auto stage_x16 = [&](int buf) {
+    const int row = tid >> 6;
+    const unsigned base = (unsigned)(OFF_X16 + myrep * REPL_X16 + (size_t)buf * MAXR * (H / 2) * 4);
+    u32x4_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      v[k] = row < R ? bld_c(wsr, base + (unsigned)(row * (H / 2)) * 4 + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      *(u32x4_t*)&s.a.xa[row][(lane + 64 * k) * 8] = v[k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = __uint_as_float(v[k][e] << 16), hi = __uint_as_float(v[k][e] & 0xFFFF0000u);
+        ss += lo * lo + hi * hi;
+      }
+    }
+    ss = wave_sum_dpp(ss);
+    if (lane == 0) s.rs[row] = rsqrtf(ss / (float)H + p.eps);
+    cons_sync(cb, cg, pk.spin, err);
+  };
+  // (wave 0, owner) the split-K pair's partial of (row 4 lk + i, column lm) in, summed with this block's, + the
+  // residual slice; returns through s.xo
+  auto pair_in = [&](f32x4_t v, int kind, unsigned tag) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = lk * 4 + i;
+      if (rr < R) {
+        const u64* g = gpart + (((size_t)kind * 128 + ot) * MAXR + rr) * 16 + lm;
+        u64 x = ld_g(g);
+        for (int spins = 0; (unsigned)(x >> 32) != tag; ++spins) {
+          if (spins > pk.spin) { atomicOr(err, 1); break; }
+          __builtin_amdgcn_s_sleep(1);
+          x = ld_g(g);
+        }
+        s.xo[rr][lm] += v[i] + __uint_as_float((unsigned)x);
+      }
+    }
+  };
+  auto pair_out = [&](f32x4_t v, int kind, unsigned tag) {  // (wave 0, odd block) this block's partial to the owner
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = lk * 4 + i;
+      if (rr < R) st_g(gpart + (((size_t)kind * 128 + ot) * MAXR + rr) * 16 + lm, __float_as_uint(v[i]), tag);
+    }
+  };
+  // (wave 0, owner) the owned slice's bf16 copy to x16 buffer `buf` of every replica, drain, flags
+  auto publish_x16 = [&](int buf, unsigned tag) {
+    const int rr = lane >> 3, pp = lane & 7;  // 8 rows x 8 column pairs
+    if (rr < R) {
+      const unsigned v = pack2bf(s.xo[rr][2 * pp], s.xo[rr][2 * pp + 1]);
+      const unsigned o = (unsigned)OFF_X16 + (unsigned)(((buf * MAXR + rr) * (H / 2)) + 8 * ot + pp) * 4;
+#pragma unroll
+      for (int rp = 0; rp < NREPL; ++rp) bst_c(v, wsr, o + rp * (unsigned)REPL_X16);
+    }
+    drain_stores();
+    if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, buf == 0 ? FL_X1 : FL_X2)) + ot, tag);
+  };
+  auto afrag = [&](const bf16_t* row0, int ld, int nrows, int kt) {  // A fragment of k tile kt from staged rows
+    return *(const u32x4_t*)(lm < nrows ? row0 + (size_t)lm * ld + kt * 32 + lk * 8 : &s.zero[lk * 8]);
+  };
+
+  // the owner's residual slice (fp32, 8 rows x 16) and this block's attention rows (K half), staged up front
+  if (owner && tid < MAXR * 16) {
+    const int rr = tid >> 4, c = tid & 15;
+    s.xo[rr][c] = rr < R ? p.x[(long long)rr * p.ldx + 16 * ot + c] : 0.f;
+  }
+  {
+    const int row = tid >> 6;  // 2 x 16 B per thread: 1024 bf16 per row
+    u32x4_t v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      v[k] = row < R ? *(const u32x4_t*)((const bf16_t*)p.att + (long long)row * p.lda + kh * (KO / 2) + (lane + 64 * k) * 8)
+                     : u32x4_t{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) *(u32x4_t*)&s.a.aa[row][(lane + 64 * k) * 8] = v[k];
+  }
+  cons_sync(cb, cg, pk.spin, err);
+  TT_STAMP(1);
+  // ------------------------------------------------------------------ o_proj (K half) + residual
+  {
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < S_O; ++j) {
+      u32x4_t f0, f1;
+      take(f0, f1);
+      const int kt = SLOT * j + 2 * w;
+      acc = mfma(afrag(&s.a.aa[0][0], ALD, R, kt), f0, acc);
+      acc = mfma(afrag(&s.a.aa[0][0], ALD, R, kt + 1), f1, acc);
+    }
+    red_put(0, acc);
+    cons_sync(cb, cg, pk.spin, err);
+    if (w == 0) {
+      const f32x4_t v = red_sum(0);
+      if (owner) {
+        pair_in(v, 0, tagof(E_PO));
+        publish_x16(0, tagof(E_X1));
+      } else {
+        pair_out(v, 0, tagof(E_PO));
+      }
+    }
+    TT_STAMP(2);
+  }
+  // ------------------------------------------------------------------ gate/up (3 tiles) + SwiGLU
+  {
+    pretake(NPRE);
+    wait_flags(fl_off(myrep, FL_X1), 128, tagof(E_X1));
+    TT_STAMP(3);
+    stage_x16(0);
+    TT_STAMP(4);
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        u32x4_t f0, f1;
+        frags(4 * t3 + j, f0, f1);
+        const int kt = SLOT * j + 2 * w;
+        acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt), f0, acc);
+        acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
+      }
+      red_put(t3 & 1, acc);
+      cons_sync(cb, cg, pk.spin, err);
+      if (w == 0 && lane < MAXR * 4) {  // SwiGLU of (row rr, column pair pp) of tile b + 256 t3
+        const int rr = lane >> 2, pp = lane & 3;
+        const int ml = (rr >> 2) * 16 + 2 * pp, e = rr & 3;
+        float g0 = 0.f, g1 = 0.f, u0 = 0.f, u1 = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NWC; ++ww) {
+          g0 += s.red[t3 & 1][ww][ml][e]; g1 += s.red[t3 & 1][ww][ml + 1][e];
+          u0 += s.red[t3 & 1][ww][ml + 8][e]; u1 += s.red[t3 & 1][ww][ml + 9][e];
+        }
+        const float rsv = s.rs[rr];
+        s.hb[t3][rr][pp] = pack2bf(silu_f(g0 * rsv) * (u0 * rsv), silu_f(g1 * rsv) * (u1 * rsv));
+      }
+    }
+    if (w == 0) {  // this block's 3 tiles x 8 rows x 4 pairs to every replica, drain, flags
+      for (int q = lane; q < 3 * MAXR * 4; q += 64) {
+        const int t3 = q / (MAXR * 4), rr = (q >> 2) % MAXR, pp = q & 3;
+        if (rr < R) {
+          const unsigned o = (unsigned)OFF_H + (unsigned)(rr * (I / 2) + (b + NB * t3) * 4 + pp) * 4;
+#pragma unroll
+          for (int rp = 0; rp < NREPL; ++rp) bst_c(s.hb[t3][rr][pp], wsr, o + rp * (unsigned)REPL_H);
+        }
+      }
+      drain_stores();
+      if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, FL_H)) + b, tagof(E_H));
+    }
+    TT_STAMP(5);
+  }
+  // ------------------------------------------------------------------ down (K half) + residual
+  {
+    pretake(S_D);
+    wait_flags(fl_off(myrep, FL_H), NB, tagof(E_H));
+    TT_STAMP(6);
+    {  // the SwiGLU rows' K half: thread -> row tid / 64, 6 x 16 B
+      const int row = tid >> 6;
+      const unsigned base = (unsigned)(OFF_H + myrep * REPL_H) + (unsigned)(row * (I / 2) + kh * (I / 4)) * 4;
+      u32x4_t v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = row < R ? bld_c(wsr, base + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) *(u32x4_t*)&s.a.ha[row][(lane + 64 * k) * 8] = v[k];
+    }
+    cons_sync(cb, cg, pk.spin, err);
+    TT_STAMP(7);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < S_D; ++j) {
+      u32x4_t f0, f1;
+      frags(j, f0, f1);
+      const int kt = SLOT * j + 2 * w;
+      acc = mfma(afrag(&s.a.ha[0][0], HLD, R, kt), f0, acc);
+      acc = mfma(afrag(&s.a.ha[0][0], HLD, R, kt + 1), f1, acc);
+    }
+    red_put(0, acc);
+    cons_sync(cb, cg, pk.spin, err);
+    if (w == 0) {
+      const f32x4_t v = red_sum(0);
+      if (owner) {
+        pair_in(v, 1, tagof(E_PD));
+        // the layer's output rows (fp32) for the next attention's residual / the final norm
+        for (int q = lane; q < MAXR * 16; q += 64) {
+          const int rr = q >> 4, c = q & 15;
+          if (rr < R) p.x[(long long)rr * p.ldx + 16 * ot + c] = s.xo[rr][c];
+        }
+        if (has_next) publish_x16(1, tagof(E_X2));
+      } else {
+        pair_out(v, 1, tagof(E_PD));
+      }
+    }
+    TT_STAMP(8);
+  }
+  // ------------------------------------------------------------------ next layer's q/k/v (input RMSNorm folded)
+  if (has_next) {
+    pretake(S_Q);
+    wait_flags(fl_off(myrep, FL_X2), 128, tagof(E_X2));
+    stage_x16(1);
+    TT_STAMP(9);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < S_Q; ++j) {
+      u32x4_t f0, f1;
+      frags(j, f0, f1);
+      const int kt = SLOT * j + 2 * w;
+      acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt), f0, acc);
+      acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
+    }
+    red_put(0, acc);
+    cons_sync(cb, cg, pk.spin, err);
+    if (w == 0) {
+      const f32x4_t v = red_sum(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = lk * 4 + i;
+        if (rr < R) p.qkv[(long long)rr * p.ldq + 16 * b + lm] = v[i] * s.rs[rr];
+      }
+    }
+  }
+  // the launch counter: every block read it before publishing, and block 0 has consumed an edge (the SwiGLU rows)
+  // from every block by now
+  if (b == 0 && tid == 0)
+    __hip_atomic_store((unsigned*)(ws + OFF_EPOCH), ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  TT_STAMP(10);
+}
+
+bool tail_resident() {
+  static int cap[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)talker_tail_k, NT, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+    cap[dev] = std::max(1, per_cu * cus);
+  }
+  return cap[dev] >= NB;
+}
+
+}  // namespace
+
+extern "C" long long qt_talker_tail_ws_bytes(void) { return (long long)WS_BYTES; }
+extern "C" long long qt_talker_tail_stamp_bytes(void) { return (long long)STAMP_BYTES; }
+
+extern "C" int qt_talker_tail_supported(int H_, int I_, int Hq, int D_, int qkv_w) {
+  return H_ == H && I_ == I && Hq * D_ == KO && qkv_w == NQKV && tail_resident();
+}
+
+extern "C" int qt_talker_tail(const qt_talker_tail_args* a, void* stream) {
+  if (!a || a->R < 1 || a->R > MAXR) return QT_ERR_SHAPE;
+  if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->att || !a->x || !a->w_o || !a->w_gu || !a->w_down)
+    return QT_ERR_ARG;
+  if (a->w_qkv_next && !a->qkv) return QT_ERR_ARG;
+  if (a->lda < KO || a->ldx < H || (a->w_qkv_next && a->ldq < NQKV)) return QT_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(a->att) | (a->lda * 2)) & 15) return QT_ERR_ARG;  // 16-byte row loads
+  if (!tail_resident()) return QT_ERR_SHAPE;
+  static const int spin = std::max(1000, qt_knob("QT_TT_SPIN", 200000));
+  hipLaunchKernelGGL(talker_tail_k, dim3(NB), dim3(NT), 0, (hipStream_t)stream, TP{*a, spin});
+  return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
+}

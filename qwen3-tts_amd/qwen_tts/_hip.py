@@ -82,6 +82,12 @@ class CpStepArgs(ctypes.Structure):
                 ("ws_bytes", c_ll)]
 
 
+class TalkerTailArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("eps", ctypes.c_float), ("att", c_void_p), ("lda", c_ll), ("x", c_void_p), ("ldx", c_ll),
+                ("w_o", c_void_p), ("w_gu", c_void_p), ("w_down", c_void_p), ("w_qkv_next", c_void_p),
+                ("qkv", c_void_p), ("ldq", c_ll), ("ws", c_void_p), ("ws_bytes", c_ll)]
+
+
 class SampleArgs(ctypes.Structure):
     _fields_ = [("logits", c_void_p), ("R", c_int), ("V", c_int), ("ld", c_ll), ("seen", c_void_p),
                 ("rep_penalty", c_float), ("n_generated", c_void_p), ("min_new_tokens", c_int), ("eos_id", c_int),
@@ -101,6 +107,7 @@ EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decod
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
            "qt_cp_step", "qt_cp_step_ws_bytes", "qt_cp_step_supported", "qt_cp_step_dbg_bytes",
+           "qt_talker_tail", "qt_talker_tail_ws_bytes", "qt_talker_tail_stamp_bytes", "qt_talker_tail_supported",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -162,6 +169,8 @@ def load_library(path: str = LIB_PATH):
         "qt_attn_oproj_resident_blocks": [],
         "qt_cp_step": [P, P], "qt_cp_step_ws_bytes": [], "qt_cp_step_dbg_bytes": [],
         "qt_cp_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+        "qt_talker_tail": [P, P], "qt_talker_tail_ws_bytes": [], "qt_talker_tail_stamp_bytes": [],
+        "qt_talker_tail_supported": [c_int, c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],

@@ -306,6 +306,30 @@ def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, s
     check(_hip.lib().qt_cp_step(ctypes.byref(a), stream()), "qt_cp_step")
 
 
+def talker_tail_ws_bytes():
+    return int(_hip.lib().qt_talker_tail_ws_bytes())
+
+
+def talker_tail_supported(H, I, Hq, D, qkv_w) -> bool:
+    return bool(_hip.lib().qt_talker_tail_supported(H, I, Hq, D, qkv_w))
+
+
+def talker_tail(att, x, R, layer, next_layer, qkv, eps, ws):
+    """qt_talker_tail: o_proj + residual -> gate/up + SwiGLU -> down + residual -> (next_layer given) its q/k/v rows, in
+    one persistent launch.  att bf16 [R][Hq*D] attention rows; x fp32 [R][H] residual rows (updated in place); qkv fp32
+    [R][qkv] out; layer / next_layer: the talker's _Layer objects.  ws: zeroed uint8 scratch of talker_tail_ws_bytes()
+    kept across launches (word 0: the sticky hand-off error flag)."""
+    a = _hip.TalkerTailArgs()
+    a.R, a.eps = R, eps
+    a.att, a.lda = ptr(att), att.stride(0)
+    a.x, a.ldx = ptr(x), x.stride(0)
+    a.w_o, a.w_gu, a.w_down = ptr(layer.o.w), ptr(layer.gu.w), ptr(layer.down.w)
+    a.w_qkv_next = ptr(next_layer.qkv.w) if next_layer is not None else None
+    a.qkv, a.ldq = (ptr(qkv), qkv.stride(0)) if next_layer is not None else (None, 0)
+    a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    check(_hip.lib().qt_talker_tail(ctypes.byref(a), stream()), "qt_talker_tail")
+
+
 def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated=None, min_new_tokens=0, eos_id=-1,
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,

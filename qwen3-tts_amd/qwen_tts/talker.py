@@ -88,12 +88,15 @@ class _Stack:
         qkv0: scratch["qkv"] already holds layer 0's q/k/v rows (gathered by the previous step's sampler)."""
         # code-predictor decode steps: attention + o_proj + residual in one launch (qt_decode_attn_oproj)
         fused_ao = decode and scratch.get("attn_oproj", False) and meta.get("const_pos", -1) >= 0
+        # talker decode: everything after each layer's attention in one launch (qt_talker_tail), which also computes
+        # the next layer's q/k/v rows; the layer outputs go to x only (the bf16 shadow is not kept current)
+        tail = decode and not fused_ao and scratch.get("tt_ws") is not None
         if x16 is not None and R > 96 and not PF:
             x16 = None  # igemm_k writes x only (decode / skinny GEMVs and gemm_pf_k keep the shadow)
         xa = x if x16 is None else x16
         for li, L in enumerate(self.layers):
             kc, vc = kv[0][li], kv[1][li]
-            if not (qkv0 and li == 0):
+            if not (qkv0 and li == 0) and not (tail and li > 0):
                 K.gemm(xa, L.qkv, scratch["qkv"], R, self.H, self.qkv_w, rms=True, eps=self.eps)
             if fused_ao:
                 K.decode_attn_oproj(scratch["qkv"], R, self.Hq, self.Hkv, self.D, L.q_norm, L.k_norm, self.eps,
@@ -113,6 +116,10 @@ class _Stack:
                            self.sin, meta["rope_pos"], meta["row_batch"], meta["kv_pos"], scratch["q"], kc, vc, Lmax)
                 K.attention(scratch["q"], R, self.Hq, self.Hkv, self.D, kc, vc, Lmax, meta["row_batch"],
                             meta["row_start"], meta["row_len"], scratch["att"], max_keys)
+            if tail:
+                nxt = self.layers[li + 1] if li + 1 < self.n_layers else None
+                K.talker_tail(scratch["att"], x, R, L, nxt, scratch["qkv"], self.eps, scratch["tt_ws"])
+                continue
             if not fused_ao:
                 K.gemm(scratch["att"], L.o, x, R, self.Hq * self.D, self.H, epi=_hip.EPI_ADD, out2=x16)
             K.gemm(xa, L.gu, scratch["h"], R, self.H, self.I, rms=True, eps=self.eps, epi=_hip.EPI_SWIGLU)
@@ -136,6 +143,10 @@ AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
 # instead of ~21 dependent launches (bf16 mode with the layer-0 q/k/v tables, <= 8 rows); QT_CP_ENGINE=0 keeps the
 # launch chain (A/B)
 CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
+# talker decode layers: o_proj -> gate/up -> down -> next layer's q/k/v as ONE persistent launch per layer (qt_talker_tail:
+# weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
+# four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
+TALKER_TAIL = os.environ.get("QT_TALKER_TAIL", "1") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -194,16 +205,16 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     return sc
 
 
-HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step; blocks not "
-                 "co-resident?); outputs of this request are invalid (QT_AO_HS=0 / QT_CP_ENGINE=0 select the forms "
-                 "without hand-offs)")
+HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step / qt_talker_tail; "
+                 "blocks not co-resident?); outputs of this request are invalid (QT_AO_HS=0 / QT_CP_ENGINE=0 / "
+                 "QT_TALKER_TAIL=0 select the forms without hand-offs)")
 
 
 def _flag_words(s):
     """The sticky hand-off error words of a session's in-launch hand-off kernels (head-split attention + o_proj,
     the code-predictor step engine), int32 device views."""
     out = []
-    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws):
+    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws, s.sc_t.get("tt_ws")):
         if ws is not None:
             out.append(ws[:4].view(torch.int32))
     return out
@@ -380,6 +391,8 @@ class Session:
         # split-KV records + arrival counters of the talker decode attention (zeroed; every launch re-arms them)
         self.sc_t["attn_ws"] = torch.zeros(K.decode_attn_ws_bytes(B, t.Hq, t.Hkv, t.D, 8), dtype=torch.uint8,
                                            device=dev)
+        if eng.talker_tail and B <= 8:  # the talker decode-layer tail engine's hand-off workspace (zeroed once)
+            self.sc_t["tt_ws"] = torch.zeros(K.talker_tail_ws_bytes(), dtype=torch.uint8, device=dev)
         self.codes = i32(B, max_frames + 2, self.G)
         # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
         self.force = i32(B, max_frames + 2, self.G) if teacher else None
@@ -453,6 +466,10 @@ class TalkerEngine:
         c = self.cp
         self.cp_engine = (CP_ENGINE and self.cp_qkv_tabs is not None and
                           K.cp_step_supported(c.H, c.I, c.Hq, c.Hkv, c.D, c.n_layers, self.Vc))
+        # the talker decode-layer tail engine (qt_talker_tail): bf16, its shapes, all 256 workgroups resident
+        t = self.talker
+        self.talker_tail = (TALKER_TAIL and self.wdt == torch.bfloat16 and
+                            K.talker_tail_supported(t.H, t.I, t.Hq, t.D, t.qkv_w))
         self._sessions: Dict[tuple, List[Session]] = {}
         torch.cuda.synchronize()
 
