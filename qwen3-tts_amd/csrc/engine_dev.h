@@ -53,4 +53,38 @@ QT_DEV void pin4(u32x4_t* a) { asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[
 #define CE_AFTER(acc) asm volatile("" : "+v"(acc)::"memory")
 
 
+// ---- weight-ring engines (talker_tail.hip): loader waves, LDS-DMA with the non-temporal policy, consumer barrier
+QT_DEV void glds16_nt(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+QT_DEV unsigned lds_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+QT_DEV void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// The consumer waves synchronise among themselves only: the loader waves run free, so a block-wide s_barrier cannot
+// be used once they have split off.  The consumers meet through an LDS arrival counter instead (generation-counted,
+// bounded spin: a give-up sets error bit 8).
+
+struct CBar {
+  unsigned* cnt;  // LDS: arrivals
+  unsigned* gen;  // LDS: generation
+};
+template <int NWC>
+QT_DEV void cons_sync(const CBar& cb, unsigned& g, int spin, int* err) {
+  // every consumer wave's LDS writes before the barrier are visible after it: the wave's own LDS operations complete
+  // (lgkmcnt(0)) before its arrival, an LDS atomic
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int lane = threadIdx.x & 63;
+  ++g;
+  if (lane == 0) {
+    const unsigned a = __hip_atomic_fetch_add(cb.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (a == g * NWC - 1) lds_st(cb.gen, g);
+  }
+  for (int spins = 0; __builtin_amdgcn_readfirstlane(lds_ld(cb.gen)) < g; ++spins) {
+    if (spins > 64 * spin) { if (lane == 0) atomicOr(err, 8); break; }
+    __builtin_amdgcn_s_sleep(0);
+  }
+}
+
 }  // namespace qt_engine

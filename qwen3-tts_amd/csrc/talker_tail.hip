@@ -74,38 +74,6 @@ struct TLds {
   unsigned done[NWC];                           // consumer wave w has finished with sequences < done[w]
 };
 
-QT_DEV void glds16_nt(const void* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
-QT_DEV unsigned lds_ld(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-QT_DEV void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-
-// The consumer waves synchronise among themselves only: the loader waves run free, so a block-wide s_barrier cannot
-// be used once they have split off.  The consumers meet through an LDS arrival counter instead (generation-counted,
-// bounded spin: a give-up sets error bit 8).
-
-struct CBar {
-  unsigned* cnt;  // LDS: arrivals
-  unsigned* gen;  // LDS: generation
-};
-QT_DEV void cons_sync(const CBar& cb, unsigned& g, int spin, int* err) {
-  // every consumer wave's LDS writes before the barrier are visible after it: the wave's own LDS operations complete
-  // (lgkmcnt(0)) before its arrival, an LDS atomic
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const int lane = threadIdx.x & 63;
-  ++g;
-  if (lane == 0) {
-    const unsigned a = __hip_atomic_fetch_add(cb.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (a == g * NWC - 1) lds_st(cb.gen, g);
-  }
-  for (int spins = 0; __builtin_amdgcn_readfirstlane(lds_ld(cb.gen)) < g; ++spins) {
-    if (spins > 64 * spin) { if (lane == 0) atomicOr(err, 8); break; }
-    __builtin_amdgcn_s_sleep(0);
-  }
-}
-
 __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   const qt_talker_tail_args& p = pk.a;
   __shared__ TLds s;
@@ -216,7 +184,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
   };
   auto red_put = [&](int buf, f32x4_t acc) {
     s.red[buf][w][lane][0] = acc[0]; s.red[buf][w][lane][1] = acc[1];
@@ -251,24 +219,30 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
     }
     ss = wave_sum_dpp(ss);
     if (lane == 0) s.rs[row] = rsqrtf(ss / (float)H + p.eps);
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
   };
   // (wave 0, owner) the split-K pair's partial of (row 4 lk + i, column lm) in, summed with this block's, + the
   // residual slice; returns through s.xo
-  auto pair_in = [&](f32x4_t v, int kind, unsigned tag) {
+  auto pair_in = [&](f32x4_t v, int kind, unsigned tag) {  // the 4 granules of the lane in flight at once
+    const u64* g = gpart + (((size_t)kind * 128 + ot) * MAXR + lk * 4) * 16 + lm;
+    u64 x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = lk * 4 + i < R ? ld_g(g + i * 16) : ((u64)tag << 32);
+    for (int spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ok = ok && (unsigned)(x[i] >> 32) == tag;
+      if (ok) break;
+      if (spins > pk.spin) { atomicOr(err, 1); break; }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((unsigned)(x[i] >> 32) != tag) x[i] = ld_g(g + i * 16);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rr = lk * 4 + i;
-      if (rr < R) {
-        const u64* g = gpart + (((size_t)kind * 128 + ot) * MAXR + rr) * 16 + lm;
-        u64 x = ld_g(g);
-        for (int spins = 0; (unsigned)(x >> 32) != tag; ++spins) {
-          if (spins > pk.spin) { atomicOr(err, 1); break; }
-          __builtin_amdgcn_s_sleep(1);
-          x = ld_g(g);
-        }
-        s.xo[rr][lm] += v[i] + __uint_as_float((unsigned)x);
-      }
+      if (rr < R) s.xo[rr][lm] += v[i] + __uint_as_float((unsigned)x[i]);
     }
   };
   auto pair_out = [&](f32x4_t v, int kind, unsigned tag) {  // (wave 0, odd block) this block's partial to the owner
@@ -309,7 +283,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) *(u32x4_t*)&s.a.aa[row][(lane + 64 * k) * 8] = v[k];
   }
-  cons_sync(cb, cg, pk.spin, err);
+  cons_sync<NWC>(cb, cg, pk.spin, err);
   TT_STAMP(1);
   // ------------------------------------------------------------------ o_proj (K half) + residual
   {
@@ -322,7 +296,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       acc = mfma(afrag(&s.a.aa[0][0], ALD, R, kt + 1), f1, acc);
     }
     red_put(0, acc);
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
     if (w == 0) {
       const f32x4_t v = red_sum(0);
       if (owner) {
@@ -353,7 +327,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
         acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
       }
       red_put(t3 & 1, acc);
-      cons_sync(cb, cg, pk.spin, err);
+      cons_sync<NWC>(cb, cg, pk.spin, err);
       if (w == 0 && lane < MAXR * 4) {  // SwiGLU of (row rr, column pair pp) of tile b + 256 t3
         const int rr = lane >> 2, pp = lane & 3;
         const int ml = (rr >> 2) * 16 + 2 * pp, e = rr & 3;
@@ -395,7 +369,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) *(u32x4_t*)&s.a.ha[row][(lane + 64 * k) * 8] = v[k];
     }
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
     TT_STAMP(7);
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -407,7 +381,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       acc = mfma(afrag(&s.a.ha[0][0], HLD, R, kt + 1), f1, acc);
     }
     red_put(0, acc);
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
     if (w == 0) {
       const f32x4_t v = red_sum(0);
       if (owner) {
@@ -440,7 +414,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
     }
     red_put(0, acc);
-    cons_sync(cb, cg, pk.spin, err);
+    cons_sync<NWC>(cb, cg, pk.spin, err);
     if (w == 0) {
       const f32x4_t v = red_sum(0);
 #pragma unroll

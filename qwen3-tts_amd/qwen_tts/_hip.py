@@ -82,6 +82,13 @@ class CpStepArgs(ctypes.Structure):
                 ("ws_bytes", c_ll)]
 
 
+class TalkerStepArgs(ctypes.Structure):
+    _fields_ = [("R", c_int), ("n_layers", c_int), ("Lmax", c_int), ("eps", ctypes.c_float), ("wtab", c_void_p),
+                ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("kv_pos", c_void_p),
+                ("row_start", c_void_p), ("row_batch", c_void_p), ("x", c_void_p), ("ldx", c_ll), ("ws", c_void_p),
+                ("ws_bytes", c_ll)]
+
+
 class TalkerTailArgs(ctypes.Structure):
     _fields_ = [("R", c_int), ("eps", ctypes.c_float), ("att", c_void_p), ("lda", c_ll), ("x", c_void_p), ("ldx", c_ll),
                 ("w_o", c_void_p), ("w_gu", c_void_p), ("w_down", c_void_p), ("w_qkv_next", c_void_p),
@@ -108,6 +115,7 @@ EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decod
            "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
            "qt_cp_step", "qt_cp_step_ws_bytes", "qt_cp_step_supported", "qt_cp_step_dbg_bytes",
            "qt_talker_tail", "qt_talker_tail_ws_bytes", "qt_talker_tail_stamp_bytes", "qt_talker_tail_supported",
+           "qt_talker_step", "qt_talker_step_ws_bytes", "qt_talker_step_stamp_bytes", "qt_talker_step_supported",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -171,6 +179,8 @@ def load_library(path: str = LIB_PATH):
         "qt_cp_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
         "qt_talker_tail": [P, P], "qt_talker_tail_ws_bytes": [], "qt_talker_tail_stamp_bytes": [],
         "qt_talker_tail_supported": [c_int, c_int, c_int, c_int, c_int],
+        "qt_talker_step": [P, P], "qt_talker_step_ws_bytes": [], "qt_talker_step_stamp_bytes": [],
+        "qt_talker_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],
         "qt_layernorm": [P, c_ll, P, P, c_float, P, c_int, c_ll, c_int, c_int, P],

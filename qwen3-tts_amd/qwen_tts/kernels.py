@@ -306,6 +306,38 @@ def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, s
     check(_hip.lib().qt_cp_step(ctypes.byref(a), stream()), "qt_cp_step")
 
 
+def talker_step_ws_bytes():
+    return int(_hip.lib().qt_talker_step_ws_bytes())
+
+
+def talker_step_supported(H, I, Hq, Hkv, D, n_layers) -> bool:
+    return bool(_hip.lib().qt_talker_step_supported(H, I, Hq, Hkv, D, n_layers))
+
+
+def talker_step_table(layers, kcs, vcs, dev):
+    """The device pointer table qt_talker_step reads ([kind][layer]: q/k/v, o_proj, gate/up, down, q_norm, k_norm,
+    k_cache, v_cache); build once per (weights, caches)."""
+    cols = [[ptr(L.qkv.w) for L in layers], [ptr(L.o.w) for L in layers], [ptr(L.gu.w) for L in layers],
+            [ptr(L.down.w) for L in layers], [ptr(L.q_norm) for L in layers], [ptr(L.k_norm) for L in layers],
+            [ptr(k) for k in kcs], [ptr(v) for v in vcs]]
+    flat = [c or 0 for col in cols for c in col]
+    return torch.tensor(flat, dtype=torch.int64).to(dev)
+
+
+def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_start, row_batch, eps, ws):
+    """qt_talker_step: every talker decoder layer of one decode step in one persistent launch.  wtab from
+    talker_step_table(); x fp32 [R][H] input rows, overwritten with the last layer's output; the int32 row arrays
+    as qt_decode_attention takes them.  ws: zeroed uint8 scratch of talker_step_ws_bytes() kept across launches."""
+    a = _hip.TalkerStepArgs()
+    a.R, a.n_layers, a.Lmax, a.eps = R, n_layers, Lmax, eps
+    a.wtab = ptr(wtab)
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    a.rope_pos, a.kv_pos, a.row_start, a.row_batch = ptr(rope_pos), ptr(kv_pos), ptr(row_start), ptr(row_batch)
+    a.x, a.ldx = ptr(x), x.stride(0)
+    a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    check(_hip.lib().qt_talker_step(ctypes.byref(a), stream()), "qt_talker_step")
+
+
 def talker_tail_ws_bytes():
     return int(_hip.lib().qt_talker_tail_ws_bytes())
 

@@ -147,6 +147,11 @@ CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
 # weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
 # four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
 TALKER_TAIL = os.environ.get("QT_TALKER_TAIL", "1") == "1"
+# ... or the whole talker decode step (every layer, attention included) as ONE persistent launch (qt_talker_step)
+# when the frame's attention runs unsplit: measured slower than attention + qt_talker_tail per layer (39.1 vs 37.4 us
+# per layer at B = 8, 267 keys, profiles/r05_talker_step_ab.txt -- its seven in-launch hand-offs per layer cost more
+# than the boundaries they replace), so off by default; QT_TALKER_STEP=1 selects it (A/B)
+TALKER_STEP = os.environ.get("QT_TALKER_STEP", "0") == "1"
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -205,16 +210,16 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     return sc
 
 
-HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step / qt_talker_tail; "
-                 "blocks not co-resident?); outputs of this request are invalid (QT_AO_HS=0 / QT_CP_ENGINE=0 / "
-                 "QT_TALKER_TAIL=0 select the forms without hand-offs)")
+HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step / qt_talker_tail / "
+                 "qt_talker_step; blocks not co-resident?); outputs of this request are invalid (QT_AO_HS=0 / "
+                 "QT_CP_ENGINE=0 / QT_TALKER_TAIL=0 / QT_TALKER_STEP=0 select the forms without hand-offs)")
 
 
 def _flag_words(s):
     """The sticky hand-off error words of a session's in-launch hand-off kernels (head-split attention + o_proj,
     the code-predictor step engine), int32 device views."""
     out = []
-    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws, s.sc_t.get("tt_ws")):
+    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws, s.sc_t.get("tt_ws"), getattr(s, "ts_ws", None)):
         if ws is not None:
             out.append(ws[:4].view(torch.int32))
     return out
@@ -393,6 +398,11 @@ class Session:
                                            device=dev)
         if eng.talker_tail and B <= 8:  # the talker decode-layer tail engine's hand-off workspace (zeroed once)
             self.sc_t["tt_ws"] = torch.zeros(K.talker_tail_ws_bytes(), dtype=torch.uint8, device=dev)
+        # the talker decode-step engine: its hand-off workspace and the pointer table of this session's caches
+        self.ts_ws = self.ts_tab = None
+        if eng.talker_step and B <= 8:
+            self.ts_ws = torch.zeros(K.talker_step_ws_bytes(), dtype=torch.uint8, device=dev)
+            self.ts_tab = K.talker_step_table(t.layers, self.kv[0], self.kv[1], dev)
         self.codes = i32(B, max_frames + 2, self.G)
         # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
         self.force = i32(B, max_frames + 2, self.G) if teacher else None
@@ -470,6 +480,8 @@ class TalkerEngine:
         t = self.talker
         self.talker_tail = (TALKER_TAIL and self.wdt == torch.bfloat16 and
                             K.talker_tail_supported(t.H, t.I, t.Hq, t.D, t.qkv_w))
+        self.talker_step = (TALKER_STEP and self.wdt == torch.bfloat16 and
+                            K.talker_step_supported(t.H, t.I, t.Hq, t.Hkv, t.D, t.n_layers))
         self._sessions: Dict[tuple, List[Session]] = {}
         torch.cuda.synchronize()
 
@@ -587,7 +599,11 @@ class TalkerEngine:
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
-        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
+        if s.ts_tab is not None and s.meta.get("nsplit", 1) == 1:  # every layer in one persistent launch
+            K.talker_step(s.ts_tab, t.n_layers, B, s.x, s.Lmax, t.cos, t.sin, s.meta["rope_pos"], s.meta["kv_pos"],
+                          s.meta["row_start"], s.meta["row_batch"], t.eps, s.ts_ws)
+        else:
+            t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
         # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])
         K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1, step_stride=1)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
