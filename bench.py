@@ -182,6 +182,32 @@ def cp_step_entry(tts, B, Lmax=18, reps=20):
                 "keys 2..15)", bound="hbm", launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
 
 
+def talker_tail_entry(tts, B, reps=5):
+    """The talker decode-layer tail engine (talker_tail_k: o_proj, gate/up, down, next q/k/v in one launch), 28
+    launches over the talker's distinct per-layer weights captured in one graph (every launch streams its weights from
+    HBM, as in a frame).  Algorithmic bytes per launch = the four matrices' bf16 weights + the attention rows in + x
+    read and written (fp32) + the q/k/v rows out."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    t, dev = eng.talker, eng.dev
+    att = torch.randn(B, t.Hq * t.D, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, t.H, device=dev)
+    qkv = torch.empty(B, t.qkv_w, device=dev)
+    ws = torch.zeros(Kn.talker_tail_ws_bytes(), dtype=torch.uint8, device=dev)
+    nl = t.n_layers
+
+    def run():
+        for i in range(nl):
+            Kn.talker_tail(att, x, B, t.layers[i], t.layers[i + 1] if i + 1 < nl else t.layers[0], qkv, t.eps, ws)
+    us = _graph_us(run, dev, reps) / nl
+    assert int(ws[:4].view(torch.int32).item()) == 0, "talker tail hand-off flag set during the kernel-table run"
+    L0 = t.layers[0]
+    wb = sum(W.w.numel() * W.w.element_size() for W in (L0.o, L0.gu, L0.down, L0.qkv))
+    byt = int(wb + B * t.Hq * t.D * 2 + B * t.H * 8 + B * t.qkv_w * 4)
+    return dict(name="talker_tail", kernel="talker_tail_k (talker o_proj + gate/up + down + next q/k/v in one launch, "
+                "LDS weight ring)", bound="hbm", launches_per_frame=nl, avg_us=us, bytes=byt, pmc_tag="talker_tail")
+
+
 def decode_kernel_table(tts, B, L_mean):
     """Every decode kernel of a frame timed live at its production shape (B rows, bf16): per-launch time x launches per
     frame gives each kernel's share of the frame; `roofline` in the JSON line is the entry with the largest share.
@@ -195,15 +221,18 @@ def decode_kernel_table(tts, B, L_mean):
     n_cp = G - 1  # CP forwards per frame: the 2-token prefill + 14 decode steps
     # with the step engine (qt_cp_step) the 14 decode steps are one launch each; the launch chain runs the prefill only
     engine = any(s.cp.ce_ws is not None for s in eng.all_sessions())
+    # with the talker tail engine the o_proj / gate-up / down GEMVs are gone and q/k/v runs for layer 0 only
+    tail = any(s.sc_t.get("tt_ws") is not None for s in eng.all_sessions())
+    n_tg = 0 if tail else t.n_layers
     n_dec = 0 if engine else n_cp - 1  # decode-step forwards on the launch chain
     tab = [
-        _gemv_entry("talker_gateup", "gemv_wt (talker MLP gate/up + SwiGLU, RMS folded)", t.n_layers,
+        _gemv_entry("talker_gateup", "gemv_wt (talker MLP gate/up + SwiGLU, RMS folded)", n_tg,
                     [L.gu for L in t.layers], B, t.H, 2 * t.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
-        _gemv_entry("talker_down", "gemv_wt (talker MLP down + residual)", t.n_layers, [L.down for L in t.layers], B,
+        _gemv_entry("talker_down", "gemv_wt (talker MLP down + residual)", n_tg, [L.down for L in t.layers], B,
                     t.I, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
-        _gemv_entry("talker_qkv", "gemv_wt (talker q/k/v, RMS folded)", t.n_layers, [L.qkv for L in t.layers], B, t.H,
+        _gemv_entry("talker_qkv", "gemv_wt (talker q/k/v, RMS folded)", 1 if tail else t.n_layers, [L.qkv for L in t.layers], B, t.H,
                     t.qkv_w, bf, torch.float32, dev, rms=True),
-        _gemv_entry("talker_o", "gemv_wt (talker o_proj + residual)", t.n_layers, [L.o for L in t.layers], B,
+        _gemv_entry("talker_o", "gemv_wt (talker o_proj + residual)", n_tg, [L.o for L in t.layers], B,
                     t.Hq * t.D, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
         _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * (1 + n_dec),
                     [L.gu for L in c.layers], B, c.H, 2 * c.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
@@ -219,6 +248,8 @@ def decode_kernel_table(tts, B, L_mean):
     ]
     if engine:
         tab.append(cp_step_entry(tts, B))
+    if tail:
+        tab.append(talker_tail_entry(tts, B))
     ra = attention_roofline(tts, B, L_mean)
     tab.append(dict(name="talker_attention", kernel=f"attn_decode_k (talker decode attention, {L_mean} keys)",
                     bound="hbm", launches_per_frame=t.n_layers, avg_us=ra["avg_us"], bytes=ra["bytes"]))
@@ -247,7 +278,7 @@ def _pmc_traffic(tag):
     return None, None
 
 
-PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj", "cp_step": "cp_step"}
+PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj", "cp_step": "cp_step", "talker_tail": "talker_tail"}
 
 
 def _rocprof_avg(tag):

@@ -13,4 +13,8 @@ for i in 1 2 3; do
   C=$(echo "FETCH_SIZE WRITE_SIZE TCP_TCC_READ_REQ_sum" | cut -d' ' -f$i)
   timeout -s KILL 120 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_cs$i -o run --output-format csv -- python3 $R/tools/pmc_cp_step.py > $R/gpurun_out/pmc$i.log 2>&1
 done
+for i in 1 2 3; do
+  C=$(echo "FETCH_SIZE WRITE_SIZE TCP_TCC_READ_REQ_sum" | cut -d' ' -f$i)
+  timeout -s KILL 180 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_tt$i -o run --output-format csv -- python3 $R/tools/pmc_talker_tail.py > $R/gpurun_out/pmct$i.log 2>&1
+done
 echo done
