@@ -104,7 +104,10 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   const int b = blockIdx.x;
   const int ot = b >> 1, kh = b & 1;
   const bool owner = kh == 0;
-  const int R = p.R, L = p.n_layers;
+  // layers [l0, l0 + L) of a LT-layer stack; qkv_in: layer l0's q/k/v rows are given (its Q phase is skipped);
+  // qkv_out: the launch ends with layer l0 + L's q/k/v rows (written to global)
+  const int R = p.R, L = p.n_layers, l0 = p.first_layer, LT = p.total_layers;
+  const bool qin = p.qkv_in != nullptr, qout = p.qkv_out != nullptr;
   char* ws = (char*)p.ws;
   int* err = (int*)(ws + OFF_ERR);
   const int myrep = b % NREPL;
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES) + b * 16 * MAXL : nullptr;
 #define TS_STAMP(l, k) \
   if (kProbe && stamps && threadIdx.x == 0) stamps[(l) * 16 + (k)] = __builtin_amdgcn_s_memrealtime();
-  const int nseq = S_L * L;
+  const int nseq = S_L * L - (qin ? S_Q : 0) + (qout ? S_Q : 0);
   // per-lane coordinates, re-derived from an opaque thread id at every layer (refresh()): otherwise hipcc hoists the
   // per-lane addresses of every phase out of the layer loop and keeps them all alive (250 VGPRs, spills)
   int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   else if (tid >= 128 && tid < 144) ((unsigned*)s.zero)[tid - 128] = 0u;
   if (tid >= 256 && tid < 256 + 8 * MAXL) {  // the per-layer pointer table
     const int k = (tid - 256) / MAXL, l = (tid - 256) % MAXL;
-    s.ptab[k][l] = l < L ? p.wtab[k * L + l] : nullptr;
+    s.ptab[k][l] = l < LT ? p.wtab[k * LT + l] : nullptr;
   }
   if (tid >= 160 && tid < 160 + 4 * MAXR) {
     const int k = (tid - 160) / MAXR, rr = (tid - 160) % MAXR;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
     const int lw = w - NWC, nwl = pk.nwl;
     if (lw >= nwl) return;
     for (int sq = lw; sq < nseq; sq += nwl) {
-      const int l = sq / S_L, j = sq % S_L;
+      const int vq = sq + (qin ? S_Q : 0), l = l0 + vq / S_L, j = vq % S_L;
       int pk_, tile, kt0, KT;
       if (j < S_Q) { pk_ = PT_QKV; tile = b; kt0 = SLOT * j; KT = KTH; }
       else if (j < S_Q + S_O) { pk_ = PT_O; tile = ot; kt0 = kh * (KTO / 2) + SLOT * (j - S_Q); KT = KTO; }
@@ -335,13 +338,10 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   }
   sync();
 
-  for (int l = 0; l < L; ++l) {
-    refresh();
-    lm = lane & 15;
-    lk = lane >> 4;
-    TS_STAMP(l, 0);
-    // ------------------------------------------------------------------ Q: q/k/v tile b (input RMSNorm folded)
-    if (l > 0) {
+  // Q: q/k/v tile b of layer l (input RMSNorm folded) from the x16 rows of the previous layer (or the staged input
+  // rows); out: the in-launch payload + flag, or the global rows of the next launch
+  auto q_phase = [&](int l, bool first, float* qkv_glob) {
+    if (!first) {
       pretake(S_Q);
       poll(fl_off(myrep, FL_X2), 128, tagof(l - 1, E_X2));
       sync();
@@ -350,20 +350,26 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
       pretake(S_Q);
     }
     TS_STAMP(l, 1);
-    {
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < S_Q; ++j) {
-        u32x4_t f0, f1;
-        frags(j, f0, f1);
-        const int kt = SLOT * j + 2 * w;
-        acc = mfma(afrag(&s.a.xa[0][0], XLD, kt), f0, acc);
-        acc = mfma(afrag(&s.a.xa[0][0], XLD, kt + 1), f1, acc);
-      }
-      red_put(0, acc);
-      sync();
-      if (w == 0) {
-        const f32x4_t v = red_sum(0);
+    for (int j = 0; j < S_Q; ++j) {
+      u32x4_t f0, f1;
+      frags(j, f0, f1);
+      const int kt = SLOT * j + 2 * w;
+      acc = mfma(afrag(&s.a.xa[0][0], XLD, kt), f0, acc);
+      acc = mfma(afrag(&s.a.xa[0][0], XLD, kt + 1), f1, acc);
+    }
+    red_put(0, acc);
+    sync();
+    if (w == 0) {
+      const f32x4_t v = red_sum(0);
+      if (qkv_glob) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = lk * 4 + i;
+          if (rr < R) qkv_glob[(long long)rr * p.ldq_out + 16 * b + lm] = v[i] * s.rs[rr];
+        }
+      } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rr = lk * 4 + i;
@@ -373,6 +379,17 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
         if (lane == 0) st_flag((unsigned*)(ws + OFF_QFL) + b, tagof(l, E_Q));
       }
     }
+  };
+
+  for (int li = 0; li < L; ++li) {
+    const int l = l0 + li;
+    refresh();
+    lm = lane & 15;
+    lk = lane >> 4;
+    TS_STAMP(l, 0);
+    const bool given = li == 0 && qin;  // this layer's q/k/v rows come from the caller
+    // ------------------------------------------------------------------ Q
+    if (!given) q_phase(l, li == 0, nullptr);
     TS_STAMP(l, 2);
     // ------------------------------------------------------------------ A: attention of (row ar, kv head ahk)
     if (attb) {
@@ -412,7 +429,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
         c0 = p.cos_tab[(long long)pos * half + lane]; s0 = p.sin_tab[(long long)pos * half + lane];
       }
       // q heads 2 ahk, 2 ahk + 1 = tiles 16 ahk .. +16, k head: 128 + 8 ahk .. +8, v head: 192 + 8 ahk .. +8
-      if (w == 0) {
+      if (w == 0 && !given) {
         const unsigned tag = tagof(l, E_Q);
         for (int spins = 0;; ++spins) {
           const int t = lane < 16 ? 16 * ahk + lane : (lane < 24 ? 128 + 8 * ahk + lane - 16 : 192 + 8 * ahk + lane - 24);
@@ -425,9 +442,15 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
       sync();
       if (w < NREP + 2) {  // q heads / new k / new v: norm + rope, the cache append
         const int hh = w < NREP ? h * NREP + w : (w == NREP ? NQ + h : NQ + NKV + h);
-        const unsigned o = (unsigned)OFF_QKV + (unsigned)(r * NQKV + hh * D) * 4;
-        float x0 = act ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(o + lane * 4), 0, SC1)) : 0.f;
-        float x1 = act ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(o + (lane + half) * 4), 0, SC1)) : 0.f;
+        float x0 = 0.f, x1 = 0.f;
+        if (given) {  // the caller's rows (written before this launch)
+          const float* src = p.qkv_in + (long long)r * p.ldq_in + hh * D;
+          if (act) { x0 = src[lane]; x1 = src[lane + half]; }
+        } else {
+          const unsigned o = (unsigned)OFF_QKV + (unsigned)(r * NQKV + hh * D) * 4;
+          x0 = act ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(o + lane * 4), 0, SC1)) : 0.f;
+          x1 = act ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(o + (lane + half) * 4), 0, SC1)) : 0.f;
+        }
         if (w <= NREP) {
           const float rs = rsqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + p.eps);
           if (act) { x0 = nw0 * (x0 * rs); x1 = nw1 * (x1 * rs); }
@@ -752,20 +775,25 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
         const f32x4_t v = red_sum(0);
         if (owner) {
           pair_in(v, 1, tagof(l, E_PD));
-          if (l + 1 < L) {
-            publish_x16(1, tagof(l, E_X2));
-          } else {  // the step's output rows
+          if (li + 1 == L) {  // the launch's output rows
             for (int q = lane; q < MAXR * 16; q += 64) {
               const int rr = q >> 4, c = q & 15;
               if (rr < R) p.x[(long long)rr * p.ldx + 16 * ot + c] = s.xo[rr][c];
             }
           }
+          if (li + 1 < L || qout) publish_x16(1, tagof(l, E_X2));
         } else {
           pair_out(v, 1, tagof(l, E_PD));
         }
       }
     }
     TS_STAMP(l, 9);
+  }
+  if (qout) {  // the next launch's q/k/v rows (layer l0 + L)
+    refresh();
+    lm = lane & 15;
+    lk = lane >> 4;
+    q_phase(l0 + L, false, p.qkv_out);
   }
   if (b == 0 && tid == 0)
     __hip_atomic_store((unsigned*)(ws + OFF_EPOCH), ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -796,7 +824,10 @@ extern "C" int qt_talker_step_supported(int H_, int I_, int Hq, int Hkv, int D_,
 }
 
 extern "C" int qt_talker_step(const qt_talker_step_args* a, void* stream) {
-  if (!a || a->R < 1 || a->R > MAXR || a->n_layers < 1 || a->n_layers > MAXL) return QT_ERR_SHAPE;
+  if (!a || a->R < 1 || a->R > MAXR || a->n_layers < 1 || a->total_layers > MAXL || a->first_layer < 0 ||
+      a->first_layer + a->n_layers > a->total_layers || (a->qkv_out && a->first_layer + a->n_layers >= a->total_layers))
+    return QT_ERR_SHAPE;
+  if ((a->qkv_in && a->ldq_in < NQKV) || (a->qkv_out && a->ldq_out < NQKV)) return QT_ERR_SHAPE;
   if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->wtab || !a->x || !a->cos_tab || !a->sin_tab ||
       !a->rope_pos || !a->kv_pos || !a->row_start || !a->row_batch)
     return QT_ERR_ARG;

@@ -324,12 +324,18 @@ def talker_step_table(layers, kcs, vcs, dev):
     return torch.tensor(flat, dtype=torch.int64).to(dev)
 
 
-def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_start, row_batch, eps, ws):
-    """qt_talker_step: every talker decoder layer of one decode step in one persistent launch.  wtab from
-    talker_step_table(); x fp32 [R][H] input rows, overwritten with the last layer's output; the int32 row arrays
-    as qt_decode_attention takes them.  ws: zeroed uint8 scratch of talker_step_ws_bytes() kept across launches."""
+def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_start, row_batch, eps, ws,
+                first_layer=0, total_layers=None, qkv_in=None, qkv_out=None):
+    """qt_talker_step: talker decoder layers [first_layer, first_layer + n_layers) of one decode step in one persistent
+    launch.  wtab from talker_step_table() (all layers); x fp32 [R][H] input rows, overwritten with the last layer's
+    output; the int32 row arrays as qt_decode_attention takes them.  qkv_in: the first layer's q/k/v rows (fp32
+    [R][4096], its projection skipped); qkv_out: also compute the next layer's q/k/v rows into it.  ws: zeroed uint8
+    scratch of talker_step_ws_bytes() kept across launches."""
     a = _hip.TalkerStepArgs()
     a.R, a.n_layers, a.Lmax, a.eps = R, n_layers, Lmax, eps
+    a.first_layer, a.total_layers = first_layer, n_layers if total_layers is None else total_layers
+    a.qkv_in, a.ldq_in = (ptr(qkv_in), qkv_in.stride(0)) if qkv_in is not None else (None, 0)
+    a.qkv_out, a.ldq_out = (ptr(qkv_out), qkv_out.stride(0)) if qkv_out is not None else (None, 0)
     a.wtab = ptr(wtab)
     a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
     a.rope_pos, a.kv_pos, a.row_start, a.row_batch = ptr(rope_pos), ptr(kv_pos), ptr(row_start), ptr(row_batch)

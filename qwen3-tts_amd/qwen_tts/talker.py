@@ -147,11 +147,12 @@ CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
 # weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
 # four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
 TALKER_TAIL = os.environ.get("QT_TALKER_TAIL", "1") == "1"
-# ... or the whole talker decode step (every layer, attention included) as ONE persistent launch (qt_talker_step)
-# when the frame's attention runs unsplit: measured slower than attention + qt_talker_tail per layer (39.1 vs 37.4 us
-# per layer at B = 8, 267 keys, profiles/r05_talker_step_ab.txt -- its seven in-launch hand-offs per layer cost more
-# than the boundaries they replace), so off by default; QT_TALKER_STEP=1 selects it (A/B)
-TALKER_STEP = os.environ.get("QT_TALKER_STEP", "0") == "1"
+# ... or qt_talker_step (attention inside the weight-ring launch) when the frame's attention runs unsplit (A/B only):
+# QT_TALKER_STEP=1 every layer in ONE launch, 2 = one launch per layer (attention .. next q/k/v, the q/k/v rows crossing
+# the boundary).  Both measured slower than attention + qt_talker_tail (B = 8, 267 keys: 39.4 / 44.7 vs 36.6 us per
+# layer, profiles/r05_talker_step_ab.txt -- in-launch hand-offs under the weight stream cost 2-5 us each, more than
+# the kernel boundaries they replace), so 0 = off is the default
+TALKER_STEP = _hip.env_int("QT_TALKER_STEP", 0)
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
@@ -403,6 +404,7 @@ class Session:
         if eng.talker_step and B <= 8:
             self.ts_ws = torch.zeros(K.talker_step_ws_bytes(), dtype=torch.uint8, device=dev)
             self.ts_tab = K.talker_step_table(t.layers, self.kv[0], self.kv[1], dev)
+            self.ts_q = [f32(B, t.qkv_w), f32(B, t.qkv_w)]  # per-layer launches: q/k/v rows in / out
         self.codes = i32(B, max_frames + 2, self.G)
         # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
         self.force = i32(B, max_frames + 2, self.G) if teacher else None
@@ -480,7 +482,7 @@ class TalkerEngine:
         t = self.talker
         self.talker_tail = (TALKER_TAIL and self.wdt == torch.bfloat16 and
                             K.talker_tail_supported(t.H, t.I, t.Hq, t.D, t.qkv_w))
-        self.talker_step = (TALKER_STEP and self.wdt == torch.bfloat16 and
+        self.talker_step = (TALKER_STEP in (1, 2) and self.wdt == torch.bfloat16 and X16 and
                             K.talker_step_supported(t.H, t.I, t.Hq, t.Hkv, t.D, t.n_layers))
         self._sessions: Dict[tuple, List[Session]] = {}
         torch.cuda.synchronize()
@@ -599,9 +601,18 @@ class TalkerEngine:
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
-        if s.ts_tab is not None and s.meta.get("nsplit", 1) == 1:  # every layer in one persistent launch
-            K.talker_step(s.ts_tab, t.n_layers, B, s.x, s.Lmax, t.cos, t.sin, s.meta["rope_pos"], s.meta["kv_pos"],
-                          s.meta["row_start"], s.meta["row_batch"], t.eps, s.ts_ws)
+        if s.ts_tab is not None and s.meta.get("nsplit", 1) == 1:
+            m = s.meta
+            if TALKER_STEP == 1:  # every layer in one persistent launch
+                K.talker_step(s.ts_tab, t.n_layers, B, s.x, s.Lmax, t.cos, t.sin, m["rope_pos"], m["kv_pos"],
+                              m["row_start"], m["row_batch"], t.eps, s.ts_ws)
+            else:  # layer 0's q/k/v, then one launch per layer (attention .. the next layer's q/k/v)
+                K.gemm(s.x16, t.layers[0].qkv, s.ts_q[0], B, t.H, t.qkv_w, rms=True, eps=t.eps)
+                for li in range(t.n_layers):
+                    K.talker_step(s.ts_tab, 1, B, s.x, s.Lmax, t.cos, t.sin, m["rope_pos"], m["kv_pos"],
+                                  m["row_start"], m["row_batch"], t.eps, s.ts_ws, first_layer=li,
+                                  total_layers=t.n_layers, qkv_in=s.ts_q[li % 2],
+                                  qkv_out=s.ts_q[(li + 1) % 2] if li + 1 < t.n_layers else None)
         else:
             t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
         # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])

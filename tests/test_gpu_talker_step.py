@@ -56,8 +56,26 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm())
 
 
-@pytest.mark.parametrize("B,n_layers", [(8, 28), (3, 4), (1, 2)])
-def test_talker_step_matches_chain(B, n_layers):
+def _run(st, B, xe, ke, ve, Lmax, meta, ws, per_layer):
+    """The engine over all layers: one launch, or one launch per layer chained through q/k/v rows (layer 0's from
+    the q/k/v GEMV on the bf16 input rows, as the frame issues it)."""
+    from qwen_tts import kernels as Kn
+    tab = Kn.talker_step_table(st.layers, ke, ve, xe.device)
+    args = (B, xe, Lmax, st.cos, st.sin, meta["rope_pos"], meta["kv_pos"], meta["row_start"], meta["row_batch"],
+            st.eps, ws)
+    if not per_layer:
+        Kn.talker_step(tab, st.n_layers, *args)
+        return
+    q = [torch.empty(B, st.qkv_w, device=xe.device) for _ in range(2)]
+    Kn.gemm(xe.to(torch.bfloat16), st.layers[0].qkv, q[0], B, st.H, st.qkv_w, rms=True, eps=st.eps)
+    for li in range(st.n_layers):
+        Kn.talker_step(tab, 1, *args, first_layer=li, total_layers=st.n_layers, qkv_in=q[li % 2],
+                       qkv_out=q[(li + 1) % 2] if li + 1 < st.n_layers else None)
+
+
+@pytest.mark.parametrize("B,n_layers,per_layer", [(8, 28, False), (3, 4, False), (1, 2, False), (8, 28, True),
+                                                  (3, 4, True)])
+def test_talker_step_matches_chain(B, n_layers, per_layer):
     from qwen_tts import kernels as Kn
     from qwen_tts.talker import _scratch
     dev = _dev()
@@ -79,9 +97,7 @@ def test_talker_step_matches_chain(B, n_layers):
     for _ in range(2):
         xe = x0.clone()
         ke, ve = [k.clone() for k in kc], [v.clone() for v in vc]
-        tab = Kn.talker_step_table(st.layers, ke, ve, dev)
-        Kn.talker_step(tab, st.n_layers, B, xe, Lmax, st.cos, st.sin, meta["rope_pos"], meta["kv_pos"],
-                       meta["row_start"], meta["row_batch"], st.eps, ws)
+        _run(st, B, xe, ke, ve, Lmax, meta, ws, per_layer)
         torch.cuda.synchronize()
         assert int(ws[:4].view(torch.int32).item()) == 0, "hand-off flag"
         outs.append((xe, ke, ve))
@@ -90,7 +106,7 @@ def test_talker_step_matches_chain(B, n_layers):
     kv_pos, rb = meta["kv_pos"].cpu(), meta["row_batch"].cpu()
     knew = torch.stack([ke[l][rb[r], :, kv_pos[r]] for l in range(n_layers) for r in range(B)]).float()
     kref = torch.stack([kr[l][rb[r], :, kv_pos[r]] for l in range(n_layers) for r in range(B)]).float()
-    print(f"\n  B={B} L={n_layers}: x rel {rel:.3e}, appended keys rel {_rel(knew, kref):.3e}")
+    print(f"\n  B={B} L={n_layers} per_layer={per_layer}: x rel {rel:.3e}, appended keys rel {_rel(knew, kref):.3e}")
     assert torch.isfinite(xe).all()
     assert rel < 2e-2
     assert _rel(knew, kref) < 2e-2
@@ -101,4 +117,4 @@ def test_talker_step_matches_chain(B, n_layers):
         assert torch.equal(ke[l].permute(0, 2, 1, 3)[mk.to(dev)], kc[l].permute(0, 2, 1, 3)[mk.to(dev)])
     x2, k2, _ = outs[1]
     assert torch.equal(x2, xe) and all(torch.equal(a, b) for a, b in zip(k2, ke))  # deterministic
-    assert int(ws[4:8].view(torch.int32).item()) == 2
+    assert int(ws[4:8].view(torch.int32).item()) == 2 * (n_layers if per_layer else 1)

@@ -43,8 +43,18 @@ def main():
         Kn.talker_step(tab, st.n_layers, B, x, Lmax, st.cos, st.sin, meta["rope_pos"], meta["kv_pos"],
                        meta["row_start"], meta["row_batch"], st.eps, ws)
 
+    q = [torch.empty(B, st.qkv_w, device=dev) for _ in range(2)]
+
+    def step_layers():
+        Kn.gemm(x16, st.layers[0].qkv, q[0], B, st.H, st.qkv_w, rms=True, eps=st.eps)
+        for li in range(st.n_layers):
+            Kn.talker_step(tab, 1, B, x, Lmax, st.cos, st.sin, meta["rope_pos"], meta["kv_pos"], meta["row_start"],
+                           meta["row_batch"], st.eps, ws, first_layer=li, total_layers=st.n_layers,
+                           qkv_in=q[li % 2], qkv_out=q[(li + 1) % 2] if li + 1 < st.n_layers else None)
+
     cases = (("chain: attention + 4 GEMVs per layer", chain), ("attention + qt_talker_tail per layer", tail),
-             ("qt_talker_step (one launch)", step)) * 2
+             ("qt_talker_step (one launch)", step), ("qt_talker_step per layer (q/k/v GEMV + 28 launches)",
+                                                    step_layers)) * 2
     if os.environ.get("TS_ONLY"):
         cases = (("qt_talker_step (one launch)", step),) * 2
     for name, fn in cases:
