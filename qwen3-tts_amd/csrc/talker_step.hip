@@ -108,6 +108,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   // qkv_out: the launch ends with layer l0 + L's q/k/v rows (written to global)
   const int R = p.R, L = p.n_layers, l0 = p.first_layer, LT = p.total_layers;
   const bool qin = p.qkv_in != nullptr, qout = p.qkv_out != nullptr;
+  const bool ain = p.att_in != nullptr, aout = p.att_out != nullptr;  // attention rows in (skip Q, A) / out (+ Q, A)
   char* ws = (char*)p.ws;
   int* err = (int*)(ws + OFF_ERR);
   const int myrep = b % NREPL;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
   u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES) + b * 16 * MAXL : nullptr;
 #define TS_STAMP(l, k) \
   if (kProbe && stamps && threadIdx.x == 0) stamps[(l) * 16 + (k)] = __builtin_amdgcn_s_memrealtime();
-  const int nseq = S_L * L - (qin ? S_Q : 0) + (qout ? S_Q : 0);
+  const int nseq = S_L * L - (qin || ain ? S_Q : 0) + (qout || aout ? S_Q : 0);
   // per-lane coordinates, re-derived from an opaque thread id at every layer (refresh()): otherwise hipcc hoists the
   // per-lane addresses of every phase out of the layer loop and keeps them all alive (250 VGPRs, spills)
   int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
     const int lw = w - NWC, nwl = pk.nwl;
     if (lw >= nwl) return;
     for (int sq = lw; sq < nseq; sq += nwl) {
-      const int vq = sq + (qin ? S_Q : 0), l = l0 + vq / S_L, j = vq % S_L;
+      const int vq = sq + (qin || ain ? S_Q : 0), l = l0 + vq / S_L, j = vq % S_L;
       int pk_, tile, kt0, KT;
       if (j < S_Q) { pk_ = PT_QKV; tile = b; kt0 = SLOT * j; KT = KTH; }
       else if (j < S_Q + S_O) { pk_ = PT_O; tile = ot; kt0 = kh * (KTO / 2) + SLOT * (j - S_Q); KT = KTO; }
@@ -381,17 +382,10 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
     }
   };
 
-  for (int li = 0; li < L; ++li) {
-    const int l = l0 + li;
-    refresh();
-    lm = lane & 15;
-    lk = lane >> 4;
-    TS_STAMP(l, 0);
-    const bool given = li == 0 && qin;  // this layer's q/k/v rows come from the caller
-    // ------------------------------------------------------------------ Q
-    if (!given) q_phase(l, li == 0, nullptr);
-    TS_STAMP(l, 2);
-    // ------------------------------------------------------------------ A: attention of (row ar, kv head ahk)
+  // A: attention of layer l for (row ar, kv head ahk), key split az; the head pair's rows go to every replica + flag
+  // (the o_proj of this launch), or to att_glob (bf16 [R][2048] of the next launch).  given: the q/k/v rows are the
+  // caller's (qkv_in), else the in-launch Q payload after its flags
+  auto a_phase = [&](int l, bool given, unsigned* att_glob) {
     if (attb) {
       AttLds& at = s.a.at;
       constexpr int LPK = D / 8, GPW = 64 / LPK, G = NWC * GPW, IC = 4;
@@ -634,7 +628,12 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
         at.out[tid] = pack2bf(res[0], res[1]);
       }
       sync();
-      if (w == 0) {  // to every replica: [K half h / 4][row r][pairs 128 (h % 4) .. + 128] (replica = [2][MAXR][512])
+      if (att_glob) {  // the next launch's attention rows: row r, pairs 128 h .. + 128
+        if (w == 0) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) att_glob[(long long)r * (p.lda_out / 2) + 128 * h + lane + 64 * k] = at.out[lane + 64 * k];
+        }
+      } else if (w == 0) {  // to every replica: [K half h / 4][row r][pairs 128 (h % 4) .. + 128] (replica = [2][MAXR][512])
         const unsigned o = (unsigned)OFF_ATT + (unsigned)(((h >> 2) * MAXR + r) * (KO / 4) + (h & 3) * (NREP * D / 2)) * 4;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -647,12 +646,27 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
       }
       }
     }
+  };
+
+  for (int li = 0; li < L; ++li) {
+    const int l = l0 + li;
+    refresh();
+    lm = lane & 15;
+    lk = lane >> 4;
+    TS_STAMP(l, 0);
+    const bool given_att = li == 0 && ain;  // this layer's attention rows come from the caller (no Q, no A)
+    const bool given = li == 0 && (qin || ain);  // this layer's q/k/v rows come from the caller
+    // ------------------------------------------------------------------ Q
+    if (!given) q_phase(l, li == 0, nullptr);
+    TS_STAMP(l, 2);
+    // ------------------------------------------------------------------ A
+    if (!given_att) a_phase(l, given, nullptr);
     TS_STAMP(l, 3);
     // ------------------------------------------------------------------ O: o_proj (K half) + residual
     pretake(S_O + 6);  // o_proj + the first 6 gate/up slots, across the attention hand-off
     {
       // producers of K half kh: the attention blocks (r, hk) with hk / 4 == kh, r < R -> flags 8 r + 4 kh .. + 4
-      if (w == 0) {
+      if (w == 0 && !given_att) {
         const unsigned tag = tagof(l, E_A);
         for (int spins = 0;; ++spins) {
           const int rr = lane >> 2, q = lane & 3;
@@ -663,13 +677,19 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
         }
       }
       sync();
-      {  // the attention rows' K half: thread -> row tid / 64, 2 x 16 B
+      {  // the attention rows' K half: thread -> row tid / 64, 2 x 16 B (the caller's rows, or the replica)
         const int row = tid >> 6;
         const unsigned base = (unsigned)(OFF_ATT + myrep * REPL_ATT) + (unsigned)kh * (unsigned)(MAXR * (KO / 4) * 4) +
                               (unsigned)(row * (KO / 4)) * 4;
         u32x4_t v[2];
+        if (given_att) {
+          const u32x4_t* src = (const u32x4_t*)((const unsigned*)p.att_in + (long long)row * (p.lda_in / 2) + kh * (KO / 4));
 #pragma unroll
-        for (int k = 0; k < 2; ++k) v[k] = row < R ? bld_c(wsr, base + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+          for (int k = 0; k < 2; ++k) v[k] = row < R ? src[lane + 64 * k] : u32x4_t{0u, 0u, 0u, 0u};
+        } else {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) v[k] = row < R ? bld_c(wsr, base + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
         for (int k = 0; k < 2; ++k) *(u32x4_t*)&s.a.aa[row][(lane + 64 * k) * 8] = v[k];
       }
@@ -781,7 +801,7 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
               if (rr < R) p.x[(long long)rr * p.ldx + 16 * ot + c] = s.xo[rr][c];
             }
           }
-          if (li + 1 < L || qout) publish_x16(1, tagof(l, E_X2));
+          if (li + 1 < L || qout || aout) publish_x16(1, tagof(l, E_X2));
         } else {
           pair_out(v, 1, tagof(l, E_PD));
         }
@@ -789,11 +809,12 @@ __global__ __launch_bounds__(NT) void talker_step_k(SP pk) {
     }
     TS_STAMP(l, 9);
   }
-  if (qout) {  // the next launch's q/k/v rows (layer l0 + L)
+  if (qout || aout) {  // the next launch's q/k/v rows (layer l0 + L), or its attention rows
     refresh();
     lm = lane & 15;
     lk = lane >> 4;
-    q_phase(l0 + L, false, p.qkv_out);
+    q_phase(l0 + L, false, aout ? nullptr : p.qkv_out);
+    if (aout) a_phase(l0 + L, false, (unsigned*)p.att_out);
   }
   if (b == 0 && tid == 0)
     __hip_atomic_store((unsigned*)(ws + OFF_EPOCH), ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -828,6 +849,10 @@ extern "C" int qt_talker_step(const qt_talker_step_args* a, void* stream) {
       a->first_layer + a->n_layers > a->total_layers || (a->qkv_out && a->first_layer + a->n_layers >= a->total_layers))
     return QT_ERR_SHAPE;
   if ((a->qkv_in && a->ldq_in < NQKV) || (a->qkv_out && a->ldq_out < NQKV)) return QT_ERR_SHAPE;
+  if ((a->att_in && (a->qkv_in || a->lda_in < KO || ((reinterpret_cast<uintptr_t>(a->att_in) | (a->lda_in * 2)) & 15))) ||
+      (a->att_out && (a->qkv_out || a->lda_out < KO || (a->lda_out & 1) ||
+                      a->first_layer + a->n_layers >= a->total_layers)))
+    return QT_ERR_SHAPE;
   if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->wtab || !a->x || !a->cos_tab || !a->sin_tab ||
       !a->rope_pos || !a->kv_pos || !a->row_start || !a->row_batch)
     return QT_ERR_ARG;

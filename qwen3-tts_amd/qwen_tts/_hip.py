@@ -87,7 +87,8 @@ class TalkerStepArgs(ctypes.Structure):
                 ("cos_tab", c_void_p), ("sin_tab", c_void_p), ("rope_pos", c_void_p), ("kv_pos", c_void_p),
                 ("row_start", c_void_p), ("row_batch", c_void_p), ("x", c_void_p), ("ldx", c_ll), ("ws", c_void_p),
                 ("ws_bytes", c_ll), ("first_layer", c_int), ("total_layers", c_int), ("qkv_in", c_void_p),
-                ("ldq_in", c_ll), ("qkv_out", c_void_p), ("ldq_out", c_ll)]
+                ("ldq_in", c_ll), ("qkv_out", c_void_p), ("ldq_out", c_ll), ("att_in", c_void_p), ("lda_in", c_ll),
+                ("att_out", c_void_p), ("lda_out", c_ll)]
 
 
 class TalkerTailArgs(ctypes.Structure):

@@ -325,7 +325,7 @@ def talker_step_table(layers, kcs, vcs, dev):
 
 
 def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_start, row_batch, eps, ws,
-                first_layer=0, total_layers=None, qkv_in=None, qkv_out=None):
+                first_layer=0, total_layers=None, qkv_in=None, qkv_out=None, att_in=None, att_out=None):
     """qt_talker_step: talker decoder layers [first_layer, first_layer + n_layers) of one decode step in one persistent
     launch.  wtab from talker_step_table() (all layers); x fp32 [R][H] input rows, overwritten with the last layer's
     output; the int32 row arrays as qt_decode_attention takes them.  qkv_in: the first layer's q/k/v rows (fp32
@@ -336,6 +336,8 @@ def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_star
     a.first_layer, a.total_layers = first_layer, n_layers if total_layers is None else total_layers
     a.qkv_in, a.ldq_in = (ptr(qkv_in), qkv_in.stride(0)) if qkv_in is not None else (None, 0)
     a.qkv_out, a.ldq_out = (ptr(qkv_out), qkv_out.stride(0)) if qkv_out is not None else (None, 0)
+    a.att_in, a.lda_in = (ptr(att_in), att_in.stride(0)) if att_in is not None else (None, 0)
+    a.att_out, a.lda_out = (ptr(att_out), att_out.stride(0)) if att_out is not None else (None, 0)
     a.wtab = ptr(wtab)
     a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
     a.rope_pos, a.kv_pos, a.row_start, a.row_batch = ptr(rope_pos), ptr(kv_pos), ptr(row_start), ptr(row_batch)

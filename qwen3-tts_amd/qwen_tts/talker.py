@@ -150,8 +150,9 @@ TALKER_TAIL = os.environ.get("QT_TALKER_TAIL", "1") == "1"
 # ... or qt_talker_step (attention inside the weight-ring launch) when the frame's attention runs unsplit (A/B only):
 # QT_TALKER_STEP=1 every layer in ONE launch, 2 = one launch per layer (attention .. next q/k/v, the q/k/v rows crossing
 # the boundary).  Both measured slower than attention + qt_talker_tail (B = 8, 267 keys: 39.4 / 44.7 vs 36.6 us per
-# layer, profiles/r05_talker_step_ab.txt -- in-launch hand-offs under the weight stream cost 2-5 us each, more than
-# the kernel boundaries they replace), so 0 = off is the default
+# layer; a third form, o_proj .. the next layer's attention per launch, 48.9: profiles/r05_talker_step_ab.txt -- in-
+# launch hand-offs under the weight stream cost 2-5 us each, more than the kernel boundaries they replace), so 0 = off
+# is the default
 TALKER_STEP = _hip.env_int("QT_TALKER_STEP", 0)
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
 X16 = os.environ.get("QT_X16", "1") == "1"

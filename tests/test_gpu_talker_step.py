@@ -66,6 +66,17 @@ def _run(st, B, xe, ke, ve, Lmax, meta, ws, per_layer):
     if not per_layer:
         Kn.talker_step(tab, st.n_layers, *args)
         return
+    if per_layer == "att":  # layer 0's q/k/v + attention on the chain, then per layer: o_proj .. next attention
+        q0 = torch.empty(B, st.qkv_w, device=xe.device)
+        Kn.gemm(xe.to(torch.bfloat16), st.layers[0].qkv, q0, B, st.H, st.qkv_w, rms=True, eps=st.eps)
+        a = [torch.empty(B, st.Hq * st.D, dtype=torch.bfloat16, device=xe.device) for _ in range(2)]
+        L0 = st.layers[0]
+        Kn.decode_attention(q0, B, st.Hq, st.Hkv, st.D, L0.q_norm, L0.k_norm, st.eps, st.cos, st.sin, meta["rope_pos"],
+                            meta["row_batch"], meta["kv_pos"], meta["row_start"], ke[0], ve[0], Lmax, a[0])
+        for li in range(st.n_layers):
+            Kn.talker_step(tab, 1, *args, first_layer=li, total_layers=st.n_layers, att_in=a[li % 2],
+                           att_out=a[(li + 1) % 2] if li + 1 < st.n_layers else None)
+        return
     q = [torch.empty(B, st.qkv_w, device=xe.device) for _ in range(2)]
     Kn.gemm(xe.to(torch.bfloat16), st.layers[0].qkv, q[0], B, st.H, st.qkv_w, rms=True, eps=st.eps)
     for li in range(st.n_layers):
@@ -74,7 +85,7 @@ def _run(st, B, xe, ke, ve, Lmax, meta, ws, per_layer):
 
 
 @pytest.mark.parametrize("B,n_layers,per_layer", [(8, 28, False), (3, 4, False), (1, 2, False), (8, 28, True),
-                                                  (3, 4, True)])
+                                                  (3, 4, True), (8, 28, "att"), (3, 4, "att")])
 def test_talker_step_matches_chain(B, n_layers, per_layer):
     from qwen_tts import kernels as Kn
     from qwen_tts.talker import _scratch

@@ -52,11 +52,24 @@ def main():
                            meta["row_batch"], st.eps, ws, first_layer=li, total_layers=st.n_layers,
                            qkv_in=q[li % 2], qkv_out=q[(li + 1) % 2] if li + 1 < st.n_layers else None)
 
+    att = [torch.empty(B, st.Hq * st.D, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+
+    def step_att():
+        Kn.gemm(x16, st.layers[0].qkv, q[0], B, st.H, st.qkv_w, rms=True, eps=st.eps)
+        L0 = st.layers[0]
+        Kn.decode_attention(q[0], B, st.Hq, st.Hkv, st.D, L0.q_norm, L0.k_norm, st.eps, st.cos, st.sin, meta["rope_pos"],
+                            meta["row_batch"], meta["kv_pos"], meta["row_start"], kc[0], vc[0], Lmax, att[0])
+        for li in range(st.n_layers):
+            Kn.talker_step(tab, 1, B, x, Lmax, st.cos, st.sin, meta["rope_pos"], meta["kv_pos"], meta["row_start"],
+                           meta["row_batch"], st.eps, ws, first_layer=li, total_layers=st.n_layers,
+                           att_in=att[li % 2], att_out=att[(li + 1) % 2] if li + 1 < st.n_layers else None)
+
     cases = (("chain: attention + 4 GEMVs per layer", chain), ("attention + qt_talker_tail per layer", tail),
+             ("qt_talker_step per layer: o_proj .. next attention", step_att),
              ("qt_talker_step (one launch)", step), ("qt_talker_step per layer (q/k/v GEMV + 28 launches)",
                                                     step_layers)) * 2
     if os.environ.get("TS_ONLY"):
-        cases = (("qt_talker_step (one launch)", step),) * 2
+        cases = (("qt_talker_step per layer: o_proj .. next attention", step_att),) * 2
     for name, fn in cases:
         us = graph_us(fn, 5, dev)
         print(f"B={B} keys={keys} {name}: {us:.1f} us per step = {us / 28:.2f} us per layer", flush=True)
