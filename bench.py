@@ -182,6 +182,33 @@ def cp_step_entry(tts, B, Lmax=18, reps=20):
                 "keys 2..15)", bound="hbm", launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
 
 
+def cp_prefill_entry(tts, B, Lmax=18, reps=20):
+    """The code predictor's 2-token prefill through the step engine (cp_step_k<1, 1>: 2B token rows, every layer +
+    lm_head[0]), one launch per frame.  Algorithmic bytes per launch = the 5 layers' weights + lm_head[0] + the K/V rows
+    written (positions 0, 1) + x and the logits."""
+    from qwen_tts import kernels as Kn
+    eng = tts.model.engine
+    c, dev = eng.cp, eng.dev
+    kc = [torch.zeros(B, c.Hkv, Lmax, c.D, device=dev, dtype=eng.kv_dtype) for _ in c.layers]
+    vc = [torch.zeros(B, c.Hkv, Lmax, c.D, device=dev, dtype=eng.kv_dtype) for _ in c.layers]
+    x = torch.randn(2 * B, c.H, device=dev)
+    logits = torch.empty(B, eng.Vc, device=dev)
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+
+    def run():
+        for _ in range(4):
+            Kn.cp_prefill(c.layers, eng.lm_heads[0], x, B, kc, vc, Lmax, c.cos, c.sin, c.eps, logits, ws)
+    us = _graph_us(run, dev, reps) / 4
+    assert int(ws[:4].view(torch.int32).item()) == 0, "cp_prefill hand-off flag set during the kernel-table run"
+    L0 = c.layers[0]
+    wb = sum(W.w.numel() * W.w.element_size() for W in (L0.qkv, L0.o, L0.gu, L0.down)) * len(c.layers)
+    lm = eng.lm_heads[0].w.numel() * eng.lm_heads[0].w.element_size()
+    kv = len(c.layers) * B * c.Hkv * c.D * kc[0].element_size() * 4
+    byt = int(wb + lm + kv + B * (2 * c.H + eng.Vc) * 4)
+    return dict(name="cp_prefill", kernel="cp_step_k<1, 1> (code-predictor 2-token prefill through the step engine)",
+                bound="hbm", launches_per_frame=1, avg_us=us, bytes=byt)
+
+
 def talker_tail_entry(tts, B, reps=5):
     """The talker decode-layer tail engine (talker_tail_k: o_proj, gate/up, down, next q/k/v in one launch), 28
     launches over the talker's distinct per-layer weights captured in one graph (every launch streams its weights from
@@ -225,6 +252,8 @@ def decode_kernel_table(tts, B, L_mean):
     tail = any(s.sc_t.get("tt_ws") is not None for s in eng.all_sessions())
     n_tg = 0 if tail else t.n_layers
     n_dec = 0 if engine else n_cp - 1  # decode-step forwards on the launch chain
+    from qwen_tts.talker import CP_PREFILL
+    n_pre = 0 if engine and CP_PREFILL else 1  # the 2-token prefill on the launch chain (else qt_cp_prefill)
     tab = [
         _gemv_entry("talker_gateup", "gemv_wt (talker MLP gate/up + SwiGLU, RMS folded)", n_tg,
                     [L.gu for L in t.layers], B, t.H, 2 * t.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
@@ -234,20 +263,22 @@ def decode_kernel_table(tts, B, L_mean):
                     t.qkv_w, bf, torch.float32, dev, rms=True),
         _gemv_entry("talker_o", "gemv_wt (talker o_proj + residual)", n_tg, [L.o for L in t.layers], B,
                     t.Hq * t.D, t.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
-        _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * (1 + n_dec),
+        _gemv_entry("cp_gateup", "gemv_wt (code-predictor gate/up + SwiGLU)", c.n_layers * (n_pre + n_dec),
                     [L.gu for L in c.layers], B, c.H, 2 * c.I, bf, bf, dev, rms=True, epi=_hip.EPI_SWIGLU),
-        _gemv_entry("cp_down", "gemv_wt (code-predictor down + residual)", c.n_layers * (1 + n_dec),
+        _gemv_entry("cp_down", "gemv_wt (code-predictor down + residual)", c.n_layers * (n_pre + n_dec),
                     [L.down for L in c.layers],
                     B, c.I, c.H, bf, torch.float32, dev, epi=_hip.EPI_ADD),
         _gemv_entry("cp_qkv", "gemv_wt (code-predictor q/k/v, layers 1-4 of decode steps + prefill)",
-                    (c.n_layers - 1) * n_dec + c.n_layers, [L.qkv for L in c.layers], B, c.H, c.qkv_w, bf,
+                    (c.n_layers - 1) * n_dec + c.n_layers * n_pre, [L.qkv for L in c.layers], B, c.H, c.qkv_w, bf,
                     torch.float32, dev, rms=True),
-        _gemv_entry("cp_lm_head", "gemv_wt (code-predictor lm_head, final norm folded)", 1 + n_dec, eng.lm_heads, B, c.H,
+        _gemv_entry("cp_lm_head", "gemv_wt (code-predictor lm_head, final norm folded)", n_pre + n_dec, eng.lm_heads, B, c.H,
                     eng.Vc, bf, torch.float32, dev, rms=True),
-        attn_oproj_entry(tts, B, n_frame=c.n_layers * (1 + n_dec)),
+        attn_oproj_entry(tts, B, n_frame=c.n_layers * (n_pre + n_dec)),
     ]
     if engine:
         tab.append(cp_step_entry(tts, B))
+        if not n_pre:
+            tab.append(cp_prefill_entry(tts, B))
     if tail:
         tab.append(talker_tail_entry(tts, B))
     ra = attention_roofline(tts, B, L_mean)

@@ -52,13 +52,19 @@ constexpr int NREPL = 8;
 constexpr size_t OFF_FLAGS = 256;                                     // [FL_QKV: NB] + [NREPL][3][NB] producer flags
 constexpr int FL_X0 = 0, FL_X1 = 1, FL_H = 2;
 constexpr size_t REPL_FLAGS = (size_t)3 * NB * 4;                     // one replica's flag block (3 KB)
-constexpr size_t OFF_QKV = OFF_FLAGS + (size_t)NB * 4 + NREPL * REPL_FLAGS;  // [NKV][MAXR][512] fp32 payload
-constexpr size_t OFF_PART = OFF_QKV + (size_t)NKV * MAXR * 512 * 4;   // [64 t][4 q][NKV][32] granules
-constexpr size_t REPL_X16 = (size_t)2 * MAXR * (H / 2) * 4;           // [2][MAXR][H/2] bf16 pairs per replica
-constexpr size_t OFF_X16 = OFF_PART + (size_t)64 * 4 * NKV * 32 * 8;  // NREPL replicas
-constexpr size_t REPL_H = (size_t)MAXR * (I / 2) * 4;                 // [MAXR][I/2] bf16 pairs per replica
-constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;                  // NREPL replicas
-constexpr size_t WS_BYTES = OFF_H + NREPL * REPL_H;
+// Payload regions for up to MR token rows (8: a decode step; 16: the 2-token prefill of 8 batch rows).  One workspace
+// serves both forms (sized for 16): every launch is ordered after the previous one on its stream.
+template <int MR>
+struct Lay {
+  static constexpr size_t OFF_QKV = OFF_FLAGS + (size_t)NB * 4 + NREPL * REPL_FLAGS;  // [NKV][MR][512] fp32 payload
+  static constexpr size_t OFF_PART = OFF_QKV + (size_t)NKV * MR * 512 * 4;   // [64 t][MR / 2 q][NKV][32] granules
+  static constexpr size_t REPL_X16 = (size_t)2 * MR * (H / 2) * 4;           // [2][MR][H/2] bf16 pairs per replica
+  static constexpr size_t OFF_X16 = OFF_PART + (size_t)64 * (MR / 2) * NKV * 32 * 8;  // NREPL replicas
+  static constexpr size_t REPL_H = (size_t)MR * (I / 2) * 4;                 // [MR][I/2] bf16 pairs per replica
+  static constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;                // NREPL replicas
+  static constexpr size_t WS = OFF_H + NREPL * REPL_H;
+};
+constexpr size_t WS_BYTES = Lay<16>::WS;
 // optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
 // fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
 constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
@@ -104,64 +110,119 @@ static_assert(offsetof(qt_cp_step_args, k_norm) == offsetof(qt_cp_step_args, w_q
 static_assert(offsetof(qt_cp_step_args, k_cache) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_KC, "pointer table");
 static_assert(offsetof(qt_cp_step_args, v_cache) == offsetof(qt_cp_step_args, w_qkv) + 8 * 8 * PT_VC, "pointer table");
 
+// MR token rows: 8 (decode: one row per batch row) or 16 (prefill: rows 2b, 2b + 1 = positions 0, 1 of batch row b).
+// A block owns MR / 8 residual slices (row pairs qo and qo + 4 in the prefill), MR / 4 rows in all.
+template <int MR>
 struct Lds {
+  static constexpr bool PF = MR == 16;
   union {
-    bf16_t xa[MAXR][XLD];  // x16 rows (all), the A operand of q/k/v, gate/up, lm_head
-    bf16_t ha[2][HLD];     // the owner's two SwiGLU rows, the A operand of down
+    bf16_t xa[MR][XLD];     // x16 rows (all), the A operand of q/k/v, gate/up, lm_head
+    bf16_t ha[MR / 4][HLD]; // the owner's SwiGLU rows, the A operand of down
   } a;
   float red[NW][64][4];                                        // per-wave MFMA partials
-  float rs[MAXR];                                              // 1 / rms per row
-  float xown[2][16];                                           // the owned residual slice
+  float rs[MR];                                                // 1 / rms per row
+  float xown[MR / 4][16];                                      // the owned residual slices
   __attribute__((aligned(16))) bf16_t zero[32];                // the A rows past the batch (MFMA rows >= R)
   const void* ptab[8][8];  // per-layer pointers [PT_*][layer]: one LDS read instead of a scalar kernarg miss per use
-  float gath[NKV][32];                                         // the 8 head partials of the owned slice
-  __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];  // attention: q as bf16 pairs
+  float gath[MR / 8][NKV][32];                                 // the 8 head partials of the owned slices
+  __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];  // decode attention: q as bf16 pairs
   __attribute__((aligned(16))) unsigned kn2[NW][D / 2];        // the new key as bf16 pairs
   float vn[NW][D];                                             // the new value (bf16-rounded)
-  __attribute__((aligned(16))) bf16_t att[NW][ALD];            // head h's attention output per row
+  // prefill attention (wave w = batch row w): q (fp32), k / v (bf16-rounded) at positions 0, 1
+  float pq[PF ? NW : 1][2][NREP][D], pkk[PF ? NW : 1][2][D], pv[PF ? NW : 1][2][D];
+  __attribute__((aligned(16))) bf16_t att[MR][ALD];            // head h's attention output per row
 };
 
 // Stage the x16 edge (all rows) into lds.a.xa and each row's 1 / rms (from the bf16 values, as the decode GEMV computes
-// it from the bf16 shadow).  Thread -> row tid / 64, pairs (tid % 64) * 8 .. + 8: the payload read is spread over all
-// eight waves' memory queues.
-QT_DEV void stage_x16(Lds& s, rsrc_t gx, unsigned base, unsigned flag_off, unsigned tag, int R, float eps, int spin,
+// it from the bf16 shadow).  Thread -> rows tid / 64 (+ 8), pairs (tid % 64) * 8 .. + 8: the payload read is spread
+// over all eight waves' memory queues.
+template <int MR>
+QT_DEV void stage_x16(Lds<MR>& s, rsrc_t gx, unsigned base, unsigned flag_off, unsigned tag, int R, float eps, int spin,
                       int* err, int tid) {
-  const int row = tid >> 6, p0 = (tid & 63) * 8;
+  constexpr int NRW = MR / 8;
+  const int p0 = (tid & 63) * 8;
   wait_flags(gx, flag_off, NB, tag, spin, err);
-  u32x4_t v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
-  if (row < R) {
-    const unsigned o = base + (unsigned)(row * (H / 2) + p0) * 4;
-    v0 = bld_c(gx, o);
-    v1 = bld_c(gx, o + 16);
-  }
-  *(u32x4_t*)&s.a.xa[row][2 * p0] = v0;
-  *(u32x4_t*)&s.a.xa[row][2 * p0 + 8] = v1;
-  float ss = 0.f;
+  u32x4_t v0[NRW], v1[NRW];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const unsigned u = k < 4 ? v0[k] : v1[k - 4];
-    const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xFFFF0000u);
-    ss += lo * lo + hi * hi;
+  for (int k = 0; k < NRW; ++k) {
+    const int row = (tid >> 6) + 8 * k;
+    v0[k] = u32x4_t{0u, 0u, 0u, 0u};
+    v1[k] = u32x4_t{0u, 0u, 0u, 0u};
+    if (row < R) {
+      const unsigned o = base + (unsigned)(row * (H / 2) + p0) * 4;
+      v0[k] = bld_c(gx, o);
+      v1[k] = bld_c(gx, o + 16);
+    }
   }
-  ss = wave_sum_dpp(ss);  // wave == row
-  if ((tid & 63) == 0) s.rs[row] = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int k = 0; k < NRW; ++k) {
+    const int row = (tid >> 6) + 8 * k;
+    *(u32x4_t*)&s.a.xa[row][2 * p0] = v0[k];
+    *(u32x4_t*)&s.a.xa[row][2 * p0 + 8] = v1[k];
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const unsigned u = q < 4 ? v0[k][q] : v1[k][q - 4];
+      const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xFFFF0000u);
+      ss += lo * lo + hi * hi;
+    }
+    ss = wave_sum_dpp(ss);  // wave == row
+    if ((tid & 63) == 0) s.rs[row] = rsqrtf(ss / (float)H + eps);
+  }
+  __syncthreads();
+}
+
+// The prefill's layer-0 input: fp32 rows of x rounded to bf16 (as the launch chain's bf16 shadow holds them), staged
+// like stage_x16 (no edge: x was written before the launch)
+QT_DEV void stage_x32(Lds<16>& s, const float* x, long long ldx, int R, float eps, int tid) {
+  const int p0 = (tid & 63) * 8;
+  f32x4_t v[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = (tid >> 6) + 8 * k;
+    const float* src = x + (long long)min(row, R - 1) * ldx + 2 * p0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[k][q] = *(const f32x4_t*)(src + 4 * q);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = (tid >> 6) + 8 * k;
+    u32x4_t a0, a1;
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float e0 = v[k][q >> 1][(q & 1) * 2], e1 = v[k][q >> 1][(q & 1) * 2 + 1];
+      const unsigned u = row < R ? pack2bf(e0, e1) : 0u;
+      if (q < 4) a0[q] = u;
+      else a1[q - 4] = u;
+      const float lo = __uint_as_float(u << 16), hi = __uint_as_float(u & 0xFFFF0000u);
+      ss += lo * lo + hi * hi;
+    }
+    *(u32x4_t*)&s.a.xa[row][2 * p0] = a0;
+    *(u32x4_t*)&s.a.xa[row][2 * p0 + 8] = a1;
+    ss = wave_sum_dpp(ss);
+    if ((tid & 63) == 0) s.rs[row] = rsqrtf(ss / (float)H + eps);
+  }
   __syncthreads();
 }
 
 // A fragment of MFMA row lm (batch row; rows >= R zero) at k tile kt from the staged x16 rows
-QT_DEV u32x4_t afrag_x(const Lds& s, int lm, int lk, int kt, int R) {
+template <int MR>
+QT_DEV u32x4_t afrag_x(const Lds<MR>& s, int lm, int lk, int kt, int R) {
   return *(const u32x4_t*)(lm < R ? &s.a.xa[lm][kt * 32 + lk * 8] : &s.zero[lk * 8]);
 }
 
 // Sum the per-wave partials of waves [w0, w0 + nw) for lane `lane` (fixed wave order)
-QT_DEV f32x4_t red_sum(const Lds& s, int w0, int nw, int lane) {
+template <int MR>
+QT_DEV f32x4_t red_sum(const Lds<MR>& s, int w0, int nw, int lane) {
   f32x4_t v = {0.f, 0.f, 0.f, 0.f};
   for (int ww = w0; ww < w0 + nw; ++ww) {
     v[0] += s.red[ww][lane][0]; v[1] += s.red[ww][lane][1]; v[2] += s.red[ww][lane][2]; v[3] += s.red[ww][lane][3];
   }
   return v;
 }
-QT_DEV void red_put(Lds& s, int w, int lane, f32x4_t acc) {
+template <int MR>
+QT_DEV void red_put(Lds<MR>& s, int w, int lane, f32x4_t acc) {
   s.red[w][lane][0] = acc[0]; s.red[w][lane][1] = acc[1]; s.red[w][lane][2] = acc[2]; s.red[w][lane][3] = acc[3];
 }
 
@@ -172,25 +233,32 @@ QT_DEV void red_put(Lds& s, int w, int lane, f32x4_t acc) {
 //    loads then return behind its own weight loads (vmcnt is in order), so every edge also waits one weight round trip;
 //  2 (ahead): one phase ahead, right after the edge that starts the previous phase (before its MFMAs): the memory
 //    pipeline has drained them by the time that phase publishes, and they have landed before the next edge's polls.
-template <int LM>
+// PF = 0: a decode step (rows = batch rows at cache position const_pos); PF = 1: the 2-token prefill (token rows 2b,
+// 2b + 1 at positions 0, 1 of batch row b; every key is new, layer 0's q/k/v computed here from x).
+template <int LM, int PF>
 __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   constexpr bool LATE = LM == 1, AHEAD = LM == 2, EARLY = LM == 0;
+  constexpr int MR = PF ? 16 : 8, NSL = MR / 8, NQO = MR / 2;
+  using LY = Lay<MR>;
   const qt_cp_step_args& p = pk.a;
-  __shared__ Lds s;
+  __shared__ Lds<MR> s;
   const int b = blockIdx.x, h = b >> 5, cg = b & 31;
-  const int to = 2 * cg + (h >> 2), qo = h & 3;  // the owned residual slice: rows 2qo, 2qo + 1, cols 16to ..
-  const int R = p.R;
+  // the owned residual slices: rows 2qo, 2qo + 1 (and 2qo + 8, 2qo + 9 in the prefill), cols 16to ..
+  const int to = 2 * cg + (h >> 2), qo = h & 3;
+  auto orow = [&](int i) { return 2 * (qo + 4 * (i >> 1)) + (i & 1); };  // token row of owned row i
+  const int R = p.R;                    // batch rows
+  const int RT = PF ? 2 * R : R;        // token rows
   char* ws = (char*)p.ws;
   int* err = (int*)(ws + OFF_ERR);
   unsigned* flags = (unsigned*)(ws + OFF_FLAGS);  // [0, NB): the q/k/v edge's flags
   const int myrep = b % NREPL;                     // the replica this block reads (its XCD under round-robin placement)
   auto fl_off = [&](int rp, int kind) { return (unsigned)(OFF_FLAGS + NB * 4 + rp * REPL_FLAGS + kind * NB * 4); };
-  u64* gpart = (u64*)(ws + OFF_PART);
+  u64* gpart = (u64*)(ws + LY::OFF_PART);
   const rsrc_t wsr = mkr(ws, (unsigned)WS_BYTES);  // payload regions, addressed by byte offset
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);  // (low word: the error flag)
-  float* dbg = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
-  u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES + DBG_BYTES) + b * 128
-                                                                              : nullptr;
+  float* dbg = !PF && p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
+  u64* stamps = !PF && p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES)
+                    ? (u64*)(ws + WS_BYTES + DBG_BYTES) + b * 128 : nullptr;
 #define CE_STAMP(k) \
   if (stamps && threadIdx.x == 0) stamps[(k)] = __builtin_amdgcn_s_memrealtime();
   CE_STAMP(0);
@@ -206,11 +274,11 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 
   {  // the owned residual slice (wave 0), the zero A row, the per-layer pointer table (wave 1)
     const int tid = threadIdx.x;
-    if (tid < 32) {
-      const int rr = 2 * qo + (tid >> 4);
-      s.xown[tid >> 4][tid & 15] = rr < R ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
-    } else if (tid < 48) {
-      ((unsigned*)s.zero)[tid - 32] = 0u;
+    if (tid < 32 * NSL) {
+      const int rr = orow(tid >> 4);
+      s.xown[tid >> 4][tid & 15] = rr < RT ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+    } else if (tid >= 128 && tid < 144) {
+      ((unsigned*)s.zero)[tid - 128] = 0u;
     } else if (tid >= 64 && tid < 128) {
       (&s.ptab[0][0])[tid - 64] = (&p.w_qkv[0])[tid - 64];
     }
@@ -238,14 +306,16 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
     const rsrc_t wo = mkr(lp(PT_O, l), (unsigned)H * NQ * D * 2);
 #pragma unroll
     for (int i = 0; i < 2; ++i) w2[i] = bld(wo, fragoff(2 * cg + f0 / 8, h * 8 + f0 % 8 + i, KTO, lane));
-    const int r = min(w, R - 1), grp = lane / LPK, sub = lane % LPK;
-    const rsrc_t kr = mkr(lp(PT_KC, l), kvbytes), vr = mkr(lp(PT_VC, l), kvbytes);
-    const unsigned kvb = (unsigned)(r * NKV + h) * kvstride + sub * 16;
+    if constexpr (!PF) {
+      const int r = min(w, R - 1), grp = lane / LPK, sub = lane % LPK;
+      const rsrc_t kr = mkr(lp(PT_KC, l), kvbytes), vr = mkr(lp(PT_VC, l), kvbytes);
+      const unsigned kvb = (unsigned)(r * NKV + h) * kvstride + sub * 16;
 #pragma unroll
-    for (int c = 0; c < IC; ++c) {
-      const unsigned o = kvb + (unsigned)min(c * GPW + grp, max(nc - 1, 0)) * D * 2;
-      kq[c] = bld(kr, o);
-      vq[c] = bld(vr, o);
+      for (int c = 0; c < IC; ++c) {
+        const unsigned o = kvb + (unsigned)min(c * GPW + grp, max(nc - 1, 0)) * D * 2;
+        kq[c] = bld(kr, o);
+        vq[c] = bld(vr, o);
+      }
     }
     CE_ISSUED();
   };
@@ -275,19 +345,30 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   // (wave 0, lane `lane`) publish the owned slice's bf16 copy (2 rows x 8 column pairs) to x16 buffer `buf` of every
   // replica, drain, then the replicas' flags
   auto publish_x16 = [&](int buf, unsigned tag, int lane) {
-    const int rr = (lane >> 3) & 1, pp = lane & 7, r0 = lane >> 4;
-    if (2 * qo + rr < R) {
-      const unsigned v = pack2bf(s.xown[rr][2 * pp], s.xown[rr][2 * pp + 1]);
-      const unsigned o = (unsigned)OFF_X16 + (unsigned)(((buf * MAXR + 2 * qo + rr) * (H / 2)) + 8 * to + pp) * 4;
-      bst_c(v, wsr, o + r0 * (unsigned)REPL_X16);
-      bst_c(v, wsr, o + (r0 + 4) * (unsigned)REPL_X16);
+    if constexpr (!PF) {
+      const int rr = (lane >> 3) & 1, pp = lane & 7, r0 = lane >> 4;
+      if (2 * qo + rr < R) {
+        const unsigned v = pack2bf(s.xown[rr][2 * pp], s.xown[rr][2 * pp + 1]);
+        const unsigned o = (unsigned)LY::OFF_X16 + (unsigned)(((buf * MR + 2 * qo + rr) * (H / 2)) + 8 * to + pp) * 4;
+        bst_c(v, wsr, o + r0 * (unsigned)LY::REPL_X16);
+        bst_c(v, wsr, o + (r0 + 4) * (unsigned)LY::REPL_X16);
+      }
+    } else {  // 2 slices x 2 rows x 8 pairs, each value by two lanes (4 replicas each)
+      const int i = (lane >> 3) & 3, pp = lane & 7, rg = lane >> 5, tr = orow(i);
+      if (tr < RT) {
+        const unsigned v = pack2bf(s.xown[i][2 * pp], s.xown[i][2 * pp + 1]);
+        const unsigned o = (unsigned)LY::OFF_X16 + (unsigned)(((buf * MR + tr) * (H / 2)) + 8 * to + pp) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bst_c(v, wsr, o + (rg * 4 + k) * (unsigned)LY::REPL_X16);
+      }
     }
     drain_stores();
     if (lane < NREPL) st_flag((unsigned*)(ws + fl_off(lane, FL_X0 + buf)) + b, tag);
   };
 
   const int L = p.n_layers;
-  load_p2(0, threadIdx.x);
+  if constexpr (PF) load_p1(lp(PT_QKV, 0), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, threadIdx.x);
+  else load_p2(0, threadIdx.x);
   for (int l = 0; l < L; ++l) {
     // per-lane coordinates from an opaque thread id: derived values are recomputed per layer, not kept alive
     int tid = threadIdx.x;
@@ -298,15 +379,17 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
     const bool pubw = w == 0;
     // ------------------------------------------------------------------ P1: q/k/v projection (layers >= 1)
     const int sb = 2 + 12 * l;
-    if (l > 0) {
+    if (l > 0 || PF) {
       CE_STAMP(sb + 0);
-      stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
-                tagof(5 * (l - 1) + 4), R, p.eps, pk.spin, err, tid);
+      if (PF && l == 0) stage_x32(*(Lds<16>*)&s, p.x, p.ldx, RT, p.eps, tid);
+      else
+        stage_x16(s, wsr, (unsigned)(LY::OFF_X16 + myrep * LY::REPL_X16) + MR * (H / 2) * 4, fl_off(myrep, FL_X1),
+                  tagof(5 * (l - 1) + 4), RT, p.eps, pk.spin, err, tid);
       CE_STAMP(sb + 1);
       if (AHEAD) load_p2(l, tid);
       u32x4_t af[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = afrag_x(s, lm, lk, w * 4 + i, R);
+      for (int i = 0; i < 4; ++i) af[i] = afrag_x(s, lm, lk, w * 4 + i, RT);
       pin4(af);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -322,9 +405,9 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rr = lk * 4 + i;
-          if (rr < R)
+          if (rr < RT)
             bst_c(__float_as_uint(v[i] * s.rs[rr]), wsr,
-                  (unsigned)OFF_QKV + (unsigned)((h * MAXR + rr) * 512 + cg * 16 + lm) * 4);
+                  (unsigned)LY::OFF_QKV + (unsigned)((h * MR + rr) * 512 + cg * 16 + lm) * 4);
         }
         CE_SUB(3);
         drain_stores();
@@ -340,6 +423,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
     }
     // ------------------------------------------------------------------ P2: attention of head h + o_proj K-slice
     {
+      if constexpr (!PF) {
       const int r = min(w, R - 1);  // wave w = row w
       const int grp = lane / LPK, sub = lane % LPK;
       const int vsel = min(grp, NREP + 1);
@@ -357,7 +441,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         load8f(p.qkv0 + (long long)r * p.ldq + (long long)hh * D + e0, xv);
       } else {
         wait_flags(wsr, (unsigned)OFF_FLAGS + h * 32 * 4, 32, tagof(5 * l), pk.spin, err);  // head h's 32 q/k/v tiles
-        const unsigned o = (unsigned)OFF_QKV + (unsigned)((h * MAXR + r) * 512 + vsel * D + e0) * 4;
+        const unsigned o = (unsigned)LY::OFF_QKV + (unsigned)((h * MR + r) * 512 + vsel * D + e0) * 4;
         const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
 #pragma unroll
         for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
@@ -460,6 +544,72 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         gm.run(m, lsum, o);
         gm.each(lane, [&](int j, int d, float ov, float lv, float) { s.att[w][j * D + d] = f2bf(ov * __builtin_amdgcn_rcpf(lv)); });
       }
+      } else {
+        // prefill: wave w = batch row w, token rows 2w (position 0) and 2w + 1 (position 1); lane group grp = q head 0,
+        // q head 1, k, v (the chain's attn_small_prefill_k: fp32 q, bf16-rounded k / v, causal softmax over <= 2 keys)
+        const int r = min(w, R - 1);
+        const int grp = lane / LPK, sub = lane % LPK;
+        const int e0 = sub * 8, half = D / 2, ec = e0 % half;
+        float nwv[8], cv[2][8], sv[2][8];
+        const float* qn = (const float*)lp(PT_QN, l);
+        const float* kn = (const float*)lp(PT_KN, l);
+        load8f((grp < NREP ? qn : kn) + e0, nwv);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          load8f(p.cos_tab + (long long)t * half + ec, cv[t]);
+          load8f(p.sin_tab + (long long)t * half + ec, sv[t]);
+        }
+        wait_flags(wsr, (unsigned)OFF_FLAGS + h * 32 * 4, 32, tagof(5 * l), pk.spin, err);  // head h's 32 q/k/v tiles
+        float xv[2][8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const unsigned o = (unsigned)LY::OFF_QKV + (unsigned)((h * MR + 2 * r + t) * 512 + grp * D + e0) * 4;
+          const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { xv[t][k] = __uint_as_float(a0[k]); xv[t][4 + k] = __uint_as_float(a1[k]); }
+        }
+        CE_STAMP(sb + 3);
+        const bool lo = e0 < half, normed = grp <= NREP;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          float ss = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ss += xv[t][i] * xv[t][i];
+          ss = group_sum_dpp<LPK>(ss);
+          const float rsn = rsqrtf(ss / (float)D + p.eps);
+          float y[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) y[i] = nwv[i] * (xv[t][i] * rsn);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float pt = half_partner<LPK>(y[i]);
+            const float ro = lo ? y[i] * cv[t][i] - pt * sv[t][i] : y[i] * cv[t][i] + pt * sv[t][i];
+            const float xo = normed ? ro : xv[t][i];
+            if (grp < NREP) s.pq[w][t][grp][e0 + i] = xo;
+            else if (grp == NREP) s.pkk[w][t][e0 + i] = bf2f(f2bf(xo));
+            else s.pv[w][t][e0 + i] = bf2f(f2bf(xo));
+          }
+        }
+        __syncthreads();
+        {  // lane group grp: token position t = grp / 2, q head j = grp % 2
+          const int t = grp >> 1, j = grp & 1;
+          const float scale = rsqrtf((float)D) * 1.4426950408889634f;
+          float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float q = s.pq[w][t][j][e0 + i];
+            d0 += q * s.pkk[w][0][e0 + i];
+            d1 += q * s.pkk[w][1][e0 + i];
+          }
+          d0 = group_sum_dpp<LPK>(d0) * scale;
+          d1 = group_sum_dpp<LPK>(d1) * scale;
+          const float mx = t ? fmaxf(d0, d1) : d0;
+          const float p0 = exp2_hw(d0 - mx), p1 = t ? exp2_hw(d1 - mx) : 0.f, den = p0 + p1;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            s.att[2 * w + t][j * D + e0 + i] = f2bf((p0 * s.pv[w][0][e0 + i] + p1 * s.pv[w][1][e0 + i]) / den);
+        }
+      }
       __syncthreads();
       CE_STAMP(sb + 4);
       if (AHEAD) load_p3(l, tid);
@@ -470,7 +620,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         const int kt0 = (2 * w) % 8;
         u32x4_t af[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = *(const u32x4_t*)(lm < NW ? &s.att[lm][(kt0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
+        for (int i = 0; i < 2; ++i) af[i] = *(const u32x4_t*)(lm < MR ? &s.att[lm][(kt0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
         asm volatile("" : "+v"(af[0]), "+v"(af[1]));
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -479,34 +629,45 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         red_put(s, w, lane, acc);
         if (EARLY && !pubw) load_p3(l, tid);
         // the new k / v of (row w, head h) into the caches (one column group appends)
-        if (cg == 0 && w < R && lane < D / 2) {
-          const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
-          ((unsigned*)lp(PT_KC, l))[o / 2 + lane] = s.kn2[w][lane];
-          ((bf16_t*)lp(PT_VC, l))[o + lane] = f2bf(s.vn[w][lane]);
-          ((bf16_t*)lp(PT_VC, l))[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
+        if constexpr (!PF) {
+          if (cg == 0 && w < R && lane < D / 2) {
+            const long long o = (((long long)w * NKV + h) * p.Lmax + kvpos) * D;
+            ((unsigned*)lp(PT_KC, l))[o / 2 + lane] = s.kn2[w][lane];
+            ((bf16_t*)lp(PT_VC, l))[o + lane] = f2bf(s.vn[w][lane]);
+            ((bf16_t*)lp(PT_VC, l))[o + lane + 64] = f2bf(s.vn[w][lane + 64]);
+          }
+        } else if (cg == 0 && w < R) {  // positions 0 and 1 of batch row w
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const long long o = (((long long)w * NKV + h) * p.Lmax + t) * D;
+            ((bf16_t*)lp(PT_KC, l))[o + lane] = f2bf(s.pkk[w][t][lane]);
+            ((bf16_t*)lp(PT_KC, l))[o + lane + 64] = f2bf(s.pkk[w][t][lane + 64]);
+            ((bf16_t*)lp(PT_VC, l))[o + lane] = f2bf(s.pv[w][t][lane]);
+            ((bf16_t*)lp(PT_VC, l))[o + lane + 64] = f2bf(s.pv[w][t][lane + 64]);
+          }
         }
       }
       __syncthreads();
       // row rr's partial for column c (thread (rr, c < 32), waves 0-3): the tile's 4 waves summed in wave order -> the
       // owner of (tile 2cg + c / 16, row pair rr / 2), as granules (data = flag: no drain)
-      if (tid < MAXR * 32) {
+      if (tid < MR * 32) {
         const int rr = tid >> 5, c = tid & 31, tt = c >> 4, cc = c & 15;
         float v = 0.f;
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) v += s.red[tt * 4 + q2][(rr >> 2) * 16 + cc][rr & 3];
-        if (rr < R)
-          st_g(gpart + ((((size_t)(2 * cg + tt) * 4 + (rr >> 1)) * NKV + h) * 32 + (rr & 1) * 16 + cc),
+        if (rr < RT)
+          st_g(gpart + ((((size_t)(2 * cg + tt) * NQO + (rr >> 1)) * NKV + h) * 32 + (rr & 1) * 16 + cc),
                __float_as_uint(v), tagof(5 * l + 1));
       }
       CE_STAMP(sb + 5);
     }
     // ------------------------------------------------------------------ residual add by the owner, x16 edge
     {
-      if (tid < NKV * 32) {  // the 8 head partials of the owned slice (granules, polled; waves 0-3)
-        const int hp = tid >> 5, sl = tid & 31;
+      if (tid < NKV * 32 * NSL) {  // the 8 head partials of the owned slices (granules, polled; waves 0-3 / 0-7)
+        const int si = tid >> 8, hp = (tid >> 5) & 7, sl = tid & 31, qq = qo + 4 * si;
         unsigned v = 0u;
-        if (2 * qo + (sl >> 4) < R) {
-          const u64* g = gpart + ((((size_t)to * 4 + qo) * NKV + hp) * 32 + sl);
+        if (2 * qq + (sl >> 4) < RT) {
+          const u64* g = gpart + ((((size_t)to * NQO + qq) * NKV + hp) * 32 + sl);
           const unsigned want = tagof(5 * l + 1);
           u64 x = ld_g(g);
           for (int spins = 0; (unsigned)(x >> 32) != want; ++spins) {
@@ -516,15 +677,15 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           }
           v = (unsigned)x;
         }
-        s.gath[hp][sl] = __uint_as_float(v);
+        s.gath[si][hp][sl] = __uint_as_float(v);
       }
       __syncthreads();
       CE_STAMP(sb + 6);
       if (pubw) {
-        if (lane < 32) {
+        if (lane < 32 * NSL) {
           float v = 0.f;
 #pragma unroll
-          for (int hp = 0; hp < NKV; ++hp) v += s.gath[hp][lane];  // head order
+          for (int hp = 0; hp < NKV; ++hp) v += s.gath[lane >> 5][hp][lane & 31];  // head order
           s.xown[lane >> 4][lane & 15] += v;
           if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
             dbg[((size_t)0 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
@@ -540,14 +701,14 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
     }
     // ------------------------------------------------------------------ P3: gate/up + SwiGLU
     {
-      stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16), fl_off(myrep, FL_X0), tagof(5 * l + 2), R, p.eps, pk.spin,
-                err, tid);
+      stage_x16(s, wsr, (unsigned)(LY::OFF_X16 + myrep * LY::REPL_X16), fl_off(myrep, FL_X0), tagof(5 * l + 2), RT, p.eps,
+                pk.spin, err, tid);
       CE_STAMP(sb + 8);
       if (AHEAD) load_p4(l, tid);
       const int k3 = ntile3 == 2 ? (w & 3) * 8 : w * 4, n3 = ntile3 == 2 ? 8 : 4;
       u32x4_t af[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = afrag_x(s, lm, lk, k3 + min(i, n3 - 1), R);
+      for (int i = 0; i < 8; ++i) af[i] = afrag_x(s, lm, lk, k3 + min(i, n3 - 1), RT);
       pin4(af);
       pin4(af + 4);
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -561,9 +722,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       __syncthreads();
       CE_SUB(14);
       if (pubw) {  // SwiGLU of (tile j, row rr, column pair pp) from the partials, every replica, drain, flags
-        const int j = lane >> 5, rr = (lane >> 2) & 7, pp = lane & 3;
+#pragma unroll
+       for (int it = 0; it < NSL; ++it) {
+        const int idx = lane + 64 * it;
+        const int j = idx / (MR * 4), rr = (idx >> 2) % MR, pp = idx & 3;
         const int tile = j == 0 ? b : b + NB, nw = ntile3 == 2 ? 4 : 8;
-        const bool mine = lane < ntile3 * MAXR * 4 && rr < R;
+        const bool mine = idx < ntile3 * MR * 4 && rr < RT;
         if (mine) {
           const int ml = (rr >> 2) * 16 + 2 * pp, e = rr & 3;  // MFMA lane of (row rr, gate column 2pp)
           float g0 = 0.f, g1 = 0.f, u0 = 0.f, u1 = 0.f;
@@ -574,14 +738,15 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           const float rsv = s.rs[rr];
           const float h0 = silu_f(g0 * rsv) * (u0 * rsv), h1 = silu_f(g1 * rsv) * (u1 * rsv);
           const unsigned hv = pack2bf(h0, h1);
-          const unsigned o = (unsigned)OFF_H + (unsigned)(rr * (I / 2) + tile * 4 + pp) * 4;
+          const unsigned o = (unsigned)LY::OFF_H + (unsigned)(rr * (I / 2) + tile * 4 + pp) * 4;
 #pragma unroll
-          for (int rp = 0; rp < NREPL; ++rp) bst_c(hv, wsr, o + rp * (unsigned)REPL_H);
+          for (int rp = 0; rp < NREPL; ++rp) bst_c(hv, wsr, o + rp * (unsigned)LY::REPL_H);
           if (dbg && l == 0) {
             dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp] = __uint_as_float(hv << 16);
             dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp + 1] = __uint_as_float(hv & 0xFFFF0000u);
           }
         }
+       }
         CE_SUB(17);
         drain_stores();
         CE_SUB(18);
@@ -599,17 +764,26 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       CE_SUB(20);
       wait_flags(wsr, fl_off(myrep, FL_H), NB, tagof(5 * l + 3), pk.spin, err);
       CE_STAMP(sb + 10);
-      {  // the owner's two SwiGLU rows: thread -> row tid / 256, pairs (tid % 256) * 6 .. + 5
-        const int rr = tid >> 8, p0 = (tid & 255) * 6;
-        uint2 v[3] = {{0u, 0u}, {0u, 0u}, {0u, 0u}};
-        if (2 * qo + rr < R) {
-          const unsigned o = (unsigned)(OFF_H + myrep * REPL_H) + (unsigned)((2 * qo + rr) * (I / 2) + p0) * 4;
+      {  // the owner's SwiGLU rows: thread -> owned row tid / 256 (+ 2), pairs (tid % 256) * 6 .. + 5
+        const int p0 = (tid & 255) * 6;
+        uint2 v[NSL][3];
 #pragma unroll
-          for (int k = 0; k < 3; ++k) v[k] = bld2_c(wsr, o + 8 * k);
+        for (int si = 0; si < NSL; ++si) {
+          const int i = (tid >> 8) + 2 * si, tr = orow(i);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) v[si][k] = uint2{0u, 0u};
+          if (tr < RT) {
+            const unsigned o = (unsigned)(LY::OFF_H + myrep * LY::REPL_H) + (unsigned)(tr * (I / 2) + p0) * 4;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) v[si][k] = bld2_c(wsr, o + 8 * k);
+          }
         }
-        uint2* hrow = (uint2*)&s.a.ha[rr][2 * p0];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) hrow[k] = v[k];
+        for (int si = 0; si < NSL; ++si) {
+          uint2* hrow = (uint2*)&s.a.ha[(tid >> 8) + 2 * si][2 * p0];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) hrow[k] = v[si][k];
+        }
       }
       CE_SUB(21);
       __syncthreads();
@@ -625,7 +799,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
         u32x4_t af[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i)
-          af[i] = *(const u32x4_t*)(lm < 2 ? &s.a.ha[lm][(w * 12 + i0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
+          af[i] = *(const u32x4_t*)(lm < 2 * NSL ? &s.a.ha[lm][(w * 12 + i0 + i) * 32 + lk * 8] : &s.zero[lk * 8]);
         pin4(af);
         asm volatile("" : "+v"(af[4]), "+v"(af[5]));
 #pragma unroll
@@ -637,7 +811,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       __syncthreads();
       CE_SUB(25);
       if (pubw) {
-        if (lane < 32) {  // (row lane / 16, column lane % 16) = MFMA row lane / 16 of MFMA lane lane % 16
+        if (lane < 32 * NSL) {  // (row lane / 16, column lane % 16) = MFMA row lane / 16 of MFMA lane lane % 16
           float v = 0.f;
 #pragma unroll
           for (int ww = 0; ww < NW; ++ww) v += s.red[ww][lane & 15][lane >> 4];
@@ -658,12 +832,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   // -------------------------------------------------------------------- final norm + lm_head[g] (tiles 0 .. V/16)
   {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lm = lane & 15, lk = lane >> 4;
-    stage_x16(s, wsr, (unsigned)(OFF_X16 + myrep * REPL_X16) + MAXR * (H / 2) * 4, fl_off(myrep, FL_X1),
-              tagof(5 * (L - 1) + 4), R, p.eps, pk.spin, err, tid);
+    stage_x16(s, wsr, (unsigned)(LY::OFF_X16 + myrep * LY::REPL_X16) + MR * (H / 2) * 4, fl_off(myrep, FL_X1),
+              tagof(5 * (L - 1) + 4), RT, p.eps, pk.spin, err, tid);
     if (b < p.V / 16) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, R), w1[i], acc);
+      for (int i = 0; i < 4; ++i) acc = mfma(afrag_x(s, lm, lk, w * 4 + i, RT), w1[i], acc);
       red_put(s, w, lane, acc);
       __syncthreads();
       if (w == 0) {
@@ -671,7 +845,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int rr = lk * 4 + i;
-          if (rr < R) p.logits[(long long)rr * p.ldl + b * 16 + lm] = v[i] * s.rs[rr];
+          // (prefill: the logits of position 1, token rows 2b + 1)
+          if (rr < RT && (!PF || (rr & 1))) p.logits[(long long)(PF ? rr >> 1 : rr) * p.ldl + b * 16 + lm] = v[i] * s.rs[rr];
         }
       }
     }
@@ -689,7 +864,8 @@ bool cp_step_resident() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
   if (cap[dev] == 0) {
     int per_cu = 1 << 20, cus = 0;  // every load-timing variant
-    for (const void* k : {(const void*)cp_step_k<0>, (const void*)cp_step_k<1>, (const void*)cp_step_k<2>}) {
+    for (const void* k : {(const void*)cp_step_k<0, 0>, (const void*)cp_step_k<1, 0>, (const void*)cp_step_k<2, 0>,
+                          (const void*)cp_step_k<1, 1>}) {
       int n = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, NT, 0) != hipSuccess) return false;
       per_cu = std::min(per_cu, n);
@@ -726,8 +902,30 @@ extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
   static const int spin = std::max(1000, qt_knob("QT_CE_SPIN", 200000));
   static const int lm = qt_knob("QT_CE_LM", 1);  // load timing (probe builds only: the product reads no env)
   const CEP pk{*a, spin};
-  if (lm == 0) hipLaunchKernelGGL(cp_step_k<0>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
-  else if (lm == 1) hipLaunchKernelGGL(cp_step_k<1>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
-  else hipLaunchKernelGGL(cp_step_k<2>, dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  if (lm == 0) hipLaunchKernelGGL((cp_step_k<0, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else if (lm == 1) hipLaunchKernelGGL((cp_step_k<1, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else hipLaunchKernelGGL((cp_step_k<2, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
+// The 2-token prefill of the same code predictor (M:1671-1675: positions 0 and 1 of every batch row -- the talker's
+// hidden state and its first code's embedding -- through all layers, their keys / values appended at cache positions 0
+// and 1, the logits of position 1 through lm_head[0]) in one launch of the same engine with 2 token rows per batch
+// row.  x: fp32 [2R][ldx] (rows 2b, 2b + 1); qkv0 / const_pos unused; logits [R][ldl].
+extern "C" int qt_cp_prefill(const qt_cp_step_args* a, void* stream) {
+  if (!a || a->R < 1 || a->R > MAXR || a->n_layers < 1 || a->n_layers > 6) return QT_ERR_SHAPE;
+  if (a->Lmax < 2 || a->V % 16 || a->V / 16 > NB || a->V <= 0) return QT_ERR_SHAPE;
+  if ((long long)a->R * NKV * a->Lmax * D * 2 >= (1ll << 31)) return QT_ERR_SHAPE;
+  if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->x || !a->logits || !a->w_lm || !a->cos_tab || !a->sin_tab)
+    return QT_ERR_ARG;
+  for (int l = 0; l < a->n_layers; ++l)
+    if (!a->w_qkv[l] || !a->w_o[l] || !a->w_gu[l] || !a->w_down[l] || !a->q_norm[l] || !a->k_norm[l] ||
+        !a->k_cache[l] || !a->v_cache[l])
+      return QT_ERR_ARG;
+  if (a->ldx % 4) return QT_ERR_SHAPE;  // 16-byte row loads
+  if (!cp_step_resident()) return QT_ERR_SHAPE;
+  static const int spin = std::max(1000, qt_knob("QT_CE_SPIN", 200000));
+  const CEP pk{*a, spin};
+  hipLaunchKernelGGL((cp_step_k<1, 1>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
   return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
 }

@@ -306,6 +306,24 @@ def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, s
     check(_hip.lib().qt_cp_step(ctypes.byref(a), stream()), "qt_cp_step")
 
 
+def cp_prefill(layers, w_lm: "Tiled", x, R, kcs, vcs, Lmax, cos, sin, eps, logits, ws):
+    """qt_cp_prefill: the code predictor's 2-token prefill (positions 0, 1 of R batch rows: x fp32 [2R][H], rows 2b,
+    2b + 1) through every layer + lm_head[0] for position 1 (logits [R][V]) in one launch of the step engine; the
+    keys / values land at cache positions 0, 1.  Same workspace as cp_step."""
+    a = _hip.CpStepArgs()
+    a.R, a.n_layers, a.Lmax, a.const_pos, a.V, a.eps = R, len(layers), Lmax, 0, w_lm.N, eps
+    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
+    for i, L in enumerate(layers):
+        a.w_qkv[i], a.w_o[i], a.w_gu[i], a.w_down[i] = ptr(L.qkv.w), ptr(L.o.w), ptr(L.gu.w), ptr(L.down.w)
+        a.q_norm[i], a.k_norm[i] = ptr(L.q_norm), ptr(L.k_norm)
+        a.k_cache[i], a.v_cache[i] = ptr(kcs[i]), ptr(vcs[i])
+    a.w_lm = ptr(w_lm.w)
+    a.x, a.ldx = ptr(x), x.stride(0)
+    a.logits, a.ldl = ptr(logits), logits.stride(0)
+    a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    check(_hip.lib().qt_cp_prefill(ctypes.byref(a), stream()), "qt_cp_prefill")
+
+
 def talker_step_ws_bytes():
     return int(_hip.lib().qt_talker_step_ws_bytes())
 

@@ -143,6 +143,9 @@ AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
 # instead of ~21 dependent launches (bf16 mode with the layer-0 q/k/v tables, <= 8 rows); QT_CP_ENGINE=0 keeps the
 # launch chain (A/B)
 CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
+# ... and the per-frame 2-token prefill through the same engine (qt_cp_prefill: 16 token rows, one launch instead of
+# ~26); QT_CP_PREFILL=0 keeps the launch chain for the prefill (A/B)
+CP_PREFILL = os.environ.get("QT_CP_PREFILL", "1") == "1"
 # talker decode layers: o_proj -> gate/up -> down -> next layer's q/k/v as ONE persistent launch per layer (qt_talker_tail:
 # weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
 # four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
@@ -634,9 +637,14 @@ class TalkerEngine:
             ln.x.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
             if ln.x16 is not None:
                 ln.x16.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
-        p16 = ln.x16 if 2 * nb <= 96 else None  # forward() keeps the shadow for decode / skinny-GEMV row counts
-        c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
-        self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
+        if ln.ce_ws is not None and CP_PREFILL:  # every layer + lm_head[0] for both positions in one launch
+            K.cp_prefill(c.layers, self.lm_heads[0], ln.x, nb, ln.kv[0], ln.kv[1], s.cp_L, c.cos, c.sin, c.eps,
+                         ln.logits, ln.ce_ws)
+            self._cp_sample(s, ln, 0)
+        else:
+            p16 = ln.x16 if 2 * nb <= 96 else None  # forward() keeps the shadow for decode / skinny-GEMV row counts
+            c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
+            self._cp_head(s, ln, ln.x.view(-1)[Hc:], 2 * Hc, 0, None if p16 is None else p16.view(-1)[Hc:])
         for g in range(1, self.G - 1):
             x = ln.x[:nb]  # written by the previous step's sampler (embedding of the token it chose)
             x16 = None if ln.x16 is None else ln.x16[:nb]

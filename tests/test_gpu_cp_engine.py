@@ -134,3 +134,64 @@ def test_cp_step_launch_sequence_on_one_workspace():
     epoch = int(ws[4:8].view(torch.int32).item())
     assert epoch == 17
     assert int(ws[:4].view(torch.int32).item()) == 0
+
+
+def _prefill_chain(st, lm, x, R, kc, vc, Lmax, dev):
+    """The launch chain of TalkerEngine._cp_lane's 2-token prefill: rows (2b, 2b + 1) at positions 0, 1 through every
+    layer (attn_small_prefill_k), then lm_head[0] on the odd rows."""
+    from qwen_tts import kernels as Kn
+    from qwen_tts.talker import _scratch
+    i32 = lambda t: t.to(torch.int32).to(dev)  # noqa: E731
+    p2 = i32(torch.arange(2 * R) % 2)
+    meta = {"rope_pos": p2, "kv_pos": p2.clone(), "row_len": p2 + 1, "row_start": i32(torch.zeros(2 * R)),
+            "row_batch": i32(torch.arange(2 * R) // 2), "small_T": 2}
+    x16 = x.to(torch.bfloat16)
+    st.forward(x, 2 * R, meta, (kc, vc), _scratch(2 * R, st, dev, attn_oproj=True), Lmax, Lmax, x16=x16)
+    logits = torch.empty(R, lm.N, device=dev)
+    Kn.gemm(x16.view(-1)[st.H:], lm, logits, R, 2 * st.H, lm.N, rms=True, eps=st.eps)
+    return logits
+
+
+@pytest.mark.parametrize("R", [8, 5, 1])
+def test_cp_prefill_matches_launch_chain(R):
+    """qt_cp_prefill (16 token rows through the step engine) against the prefill launch chain: logits of position 1
+    and the keys / values appended at positions 0, 1 within bf16 tolerance; deterministic; on a workspace shared with
+    decode steps."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    st, lm, g = _cp_stack(dev, seed=5)
+    if not Kn.cp_step_supported(st.H, st.I, st.Hq, st.Hkv, st.D, st.n_layers, lm.N):
+        pytest.skip("qt_cp_step not supported on this device")
+    Lmax = 18
+    x = torch.randn(2 * R, st.H, generator=g).to(dev)
+    kc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    vc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    kc1, vc1 = [k.clone() for k in kc], [v.clone() for v in vc]
+    ref = _prefill_chain(st, lm, x.clone(), R, kc1, vc1, Lmax, dev)
+    ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+    outs = []
+    for i in range(3):
+        if i == 1:  # a decode step in between on the same workspace
+            xd, x16d, qkv0, kcd, vcd = _inputs(st, R, Lmax, g, dev)
+            Kn.cp_step(st.layers, lm, xd, qkv0, R, kcd, vcd, Lmax, 2, st.cos, st.sin, st.eps,
+                       torch.empty(R, lm.N, device=dev), ws)
+        kc2, vc2 = [k.clone() for k in kc], [v.clone() for v in vc]
+        logits = torch.full((R, lm.N), float("nan"), device=dev)
+        Kn.cp_prefill(st.layers, lm, x, R, kc2, vc2, Lmax, st.cos, st.sin, st.eps, logits, ws)
+        torch.cuda.synchronize()
+        outs.append((logits, kc2, vc2))
+    assert int(ws[:4].view(torch.int32).item()) == 0, "hand-off poll gave up"
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0])
+    logits, kc2, vc2 = outs[0]
+    e = _rel(logits, ref)
+    print(f"\n  prefill R={R}: logits rel-L2 {e:.2e}; argmax agree {(logits.argmax(-1) == ref.argmax(-1)).float().mean():.2f}")
+    assert torch.isfinite(logits).all()
+    assert e < 2e-2
+    for li in range(st.n_layers):
+        for t in range(2):
+            assert _rel(kc2[li][:, :, t], kc1[li][:, :, t]) < 2e-2, (li, t)
+            assert _rel(vc2[li][:, :, t], vc1[li][:, :, t]) < 2e-2, (li, t)
+        assert torch.equal(kc2[li][:, :, 2:], kc1[li][:, :, 2:])  # nothing else written
+        assert torch.equal(vc2[li][:, :, 2:], vc1[li][:, :, 2:])
+    assert int(ws[4:8].view(torch.int32).item()) == 4  # 3 prefills + 1 decode step advanced the launch counter
