@@ -257,7 +257,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   const rsrc_t wsr = mkr(ws, (unsigned)WS_BYTES);  // payload regions, addressed by byte offset
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);  // (low word: the error flag)
   float* dbg = !PF && p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
-  u64* stamps = !PF && p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES)
+  u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES)
                     ? (u64*)(ws + WS_BYTES + DBG_BYTES) + b * 128 : nullptr;
 #define CE_STAMP(k) \
   if (stamps && threadIdx.x == 0) stamps[(k)] = __builtin_amdgcn_s_memrealtime();

@@ -43,7 +43,8 @@ def main():
     st.n_layers = len(all_layers)
 
 
-if __name__ == "__main__" and not (os.environ.get("CE_LAYER0") or os.environ.get("CE_STAMPS") or os.environ.get("CE_TIME")):
+if __name__ == "__main__" and not (os.environ.get("CE_LAYER0") or os.environ.get("CE_STAMPS") or os.environ.get("CE_TIME")
+                               or os.environ.get("CE_PF_STAMPS")):
     main()
 
 
@@ -173,3 +174,36 @@ def timing(R=8, reps=50):
 
 if __name__ == "__main__" and os.environ.get("CE_TIME"):
     timing()
+
+
+def pf_stamps(R=8, reps=3):
+    """Per-phase timestamps of the 2-token prefill launch (qt_cp_prefill), as stamps() (layer 0 has its q/k/v phase)."""
+    from qwen_tts import _hip
+    import numpy as np
+    dev = torch.device("cuda:0")
+    st, lm, g = _cp_stack(dev)
+    Lmax = 18
+    x = torch.randn(2 * R, st.H, generator=g).to(dev)
+    kc = [torch.zeros(R, st.Hkv, Lmax, st.D, device=dev, dtype=torch.bfloat16) for _ in st.layers]
+    vc = [torch.zeros(R, st.Hkv, Lmax, st.D, device=dev, dtype=torch.bfloat16) for _ in st.layers]
+    nws = Kn.cp_step_ws_bytes()
+    ws = torch.zeros(nws + int(_hip.lib().qt_cp_step_dbg_bytes()), dtype=torch.uint8, device=dev)
+    logits = torch.empty(R, lm.N, device=dev)
+    dbg_off = nws + 4 * 8 * 4096 * 4
+    tot = []
+    for rep in range(reps * 5):
+        Kn.cp_prefill(st.layers, lm, x, R, kc, vc, Lmax, st.cos, st.sin, st.eps, logits, ws)
+        torch.cuda.synchronize()
+        t = ws[dbg_off:].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64) * 0.01
+        t0 = t[:, 0].min()
+        tot.append(t[:, 1].max() - t0)
+    print(f"prefill launch: first block start -> last block end {t[:, 1].max() - t0:.2f} us; start spread "
+          f"{t[:, 0].max() - t0:.2f} us")
+    for l in range(st.n_layers):
+        print(f"  layer {l}: " + " | ".join(f"{n} {np.median(t[:, 2 + 12 * l + k]) - t0:6.2f}/"
+                                            f"{t[:, 2 + 12 * l + k].max() - t0:6.2f}" for k, n in enumerate(EVENTS)))
+    print(f"kernel time over {len(tot)} launches: median {np.median(tot):.2f} us, min {np.min(tot):.2f}")
+
+
+if __name__ == "__main__" and os.environ.get("CE_PF_STAMPS"):
+    pf_stamps()
