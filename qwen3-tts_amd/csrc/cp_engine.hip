@@ -29,6 +29,7 @@
 #include "common.h"
 #include "attn_dev.h"
 #include "engine_dev.h"
+#include "sample_dev.h"
 #include <algorithm>
 
 namespace {
@@ -64,7 +65,12 @@ struct Lay {
   static constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;                // NREPL replicas
   static constexpr size_t WS = OFF_H + NREPL * REPL_H;
 };
-constexpr size_t WS_BYTES = Lay<16>::WS;
+// the fused sampler's hand-off (qt_cp_step_sampled): per-row flags, the chosen tokens' x rows and layer-0 q/k/v rows
+constexpr size_t OFF_SFL = Lay<16>::WS;                     // [8] flags (256 B)
+constexpr size_t OFF_SX = OFF_SFL + 256;                    // [8][H] fp32
+constexpr size_t OFF_SQ = OFF_SX + (size_t)8 * H * 4;       // [8][(NQ + 2 NKV) D] fp32
+constexpr int E_SAMP = 30;                                  // its tag slot
+constexpr size_t WS_BYTES = OFF_SQ + (size_t)8 * (NQ + 2 * NKV) * D * 4;
 // optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
 // fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
 constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
@@ -75,6 +81,12 @@ constexpr size_t STAMP_BYTES = (size_t)NB * 128 * 8;  // + [64, 128): sub-phase 
 struct CEP {
   qt_cp_step_args a;
   int spin;
+  // qt_cp_step_sampled: the previous step's token choice at the start of this launch (sa: qt_sample's arguments with
+  // no embedding outputs; the engine gathers the rows of gx / gq itself and hands them to its blocks)
+  int fuse;
+  qt_sample_args sa;
+  const float* gx;
+  const float* gq;
 };
 
 // Wave 0 (the publishing wave) waits until the n (multiple of 4, <= 256) flag words at byte offset `off` all carry
@@ -118,7 +130,9 @@ struct Lds {
   union {
     bf16_t xa[MR][XLD];     // x16 rows (all), the A operand of q/k/v, gate/up, lm_head
     bf16_t ha[MR / 4][HLD]; // the owner's SwiGLU rows, the A operand of down
+    qt_sample_dev::SampSh samp;  // the fused sampler (layer 0, before any x16 staging)
   } a;
+  unsigned sb_cnt, sb_gen;  // the fused sampler's 4-wave barrier
   float red[NW][64][4];                                        // per-wave MFMA partials
   float rs[MR];                                                // 1 / rms per row
   float xown[MR / 4][16];                                      // the owned residual slices
@@ -247,6 +261,7 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   const int to = 2 * cg + (h >> 2), qo = h & 3;
   auto orow = [&](int i) { return 2 * (qo + 4 * (i >> 1)) + (i & 1); };  // token row of owned row i
   const int R = p.R;                    // batch rows
+  const bool fuse = !PF && pk.fuse;     // the previous step's sampler runs here first (qt_cp_step_sampled)
   const int RT = PF ? 2 * R : R;        // token rows
   char* ws = (char*)p.ws;
   int* err = (int*)(ws + OFF_ERR);
@@ -274,9 +289,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 
   {  // the owned residual slice (wave 0), the zero A row, the per-layer pointer table (wave 1)
     const int tid = threadIdx.x;
-    if (tid < 32 * NSL) {
+    if (tid < 32 * NSL) {  // (fused sampler: the rows are the chosen tokens' -- read at the first residual add)
       const int rr = orow(tid >> 4);
-      s.xown[tid >> 4][tid & 15] = rr < RT ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+      s.xown[tid >> 4][tid & 15] = rr < RT && !fuse ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
+    } else if (tid == 144) {
+      s.sb_cnt = 0u;
+      s.sb_gen = 0u;
     } else if (tid >= 128 && tid < 144) {
       ((unsigned*)s.zero)[tid - 128] = 0u;
     } else if (tid >= 64 && tid < 128) {
@@ -369,6 +387,28 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   const int L = p.n_layers;
   if constexpr (PF) load_p1(lp(PT_QKV, 0), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, threadIdx.x);
   else load_p2(0, threadIdx.x);
+  const unsigned* sfl = (const unsigned*)(ws + OFF_SFL);
+  if (fuse && b % 33 == 0 && b / 33 < R && threadIdx.x < 256) {
+    // the fused sampler of row r = b / 33 (one block per XCD), waves 0-3: qt_sample's body on the previous launch's
+    // logits (visible: kernel boundary), then the chosen token's x row and layer-0 q/k/v row to the hand-off area
+    // (write-through), drained, then the row's flag
+    const int r = b / 33, tid = threadIdx.x;
+    CBar cb{&s.sb_cnt, &s.sb_gen};
+    unsigned g = 0;
+    const int tok = qt_sample_dev::sample_row<8>(pk.sa, 0, r, tid, s.a.samp, [&]() { cons_sync<4>(cb, g, pk.spin, err); });
+    const rsrc_t tx = mkr(pk.gx + (long long)tok * H, H * 4);
+    const rsrc_t tq = mkr(pk.gq + (long long)tok * (NQ + 2 * NKV) * D, (NQ + 2 * NKV) * D * 4);
+    const u32x4_t vx = bld(tx, tid * 16);
+    u32x4_t vq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) vq[k] = bld(tq, (tid + 256 * k) * 16);
+    bst4_c(vx, wsr, (unsigned)(OFF_SX + (size_t)r * H * 4) + tid * 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bst4_c(vq[k], wsr, (unsigned)(OFF_SQ + (size_t)r * (NQ + 2 * NKV) * D * 4) + (tid + 256 * k) * 16);
+    drain_stores();
+    cons_sync<4>(cb, g, pk.spin, err);
+    if (tid == 0) st_flag((unsigned*)sfl + r, tagof(E_SAMP));
+  }
   for (int l = 0; l < L; ++l) {
     // per-lane coordinates from an opaque thread id: derived values are recomputed per layer, not kept alive
     int tid = threadIdx.x;
@@ -438,7 +478,19 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       float xv[8];
       if (l == 0) {
         const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
-        load8f(p.qkv0 + (long long)r * p.ldq + (long long)hh * D + e0, xv);
+        if (fuse) {  // row r's q/k/v from the fused sampler's hand-off
+          const unsigned want = tagof(E_SAMP);
+          for (int spins = 0; __builtin_amdgcn_readfirstlane(ld_flag(sfl + r)) != want; ++spins) {
+            if (spins > pk.spin) { if (lane == 0) atomicOr(err, 1); break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          const unsigned o = (unsigned)OFF_SQ + (unsigned)(r * (NQ + 2 * NKV) * D + hh * D + e0) * 4;
+          const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
+        } else {
+          load8f(p.qkv0 + (long long)r * p.ldq + (long long)hh * D + e0, xv);
+        }
       } else {
         wait_flags(wsr, (unsigned)OFF_FLAGS + h * 32 * 4, 32, tagof(5 * l), pk.spin, err);  // head h's 32 q/k/v tiles
         const unsigned o = (unsigned)LY::OFF_QKV + (unsigned)((h * MR + r) * 512 + vsel * D + e0) * 4;
@@ -686,6 +738,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           float v = 0.f;
 #pragma unroll
           for (int hp = 0; hp < NKV; ++hp) v += s.gath[lane >> 5][hp][lane & 31];  // head order
+          if (fuse && l == 0) {  // the residual rows: the chosen tokens' x rows (every row's flag was seen in P2)
+            const int rr = orow(lane >> 4);
+            if (rr < RT)
+              s.xown[lane >> 4][lane & 15] =
+                  __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(OFF_SX + ((size_t)rr * H + 16 * to + (lane & 15)) * 4), 0, SC1));
+          }
           s.xown[lane >> 4][lane & 15] += v;
           if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
             dbg[((size_t)0 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
@@ -876,6 +934,13 @@ bool cp_step_resident() {
   return cap[dev] >= NB;
 }
 
+static int cp_step_go(const CEP& pk, int lm, void* stream) {
+  if (lm == 0) hipLaunchKernelGGL((cp_step_k<0, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else if (lm == 1) hipLaunchKernelGGL((cp_step_k<1, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  else hipLaunchKernelGGL((cp_step_k<2, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
+  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+}
+
 }  // namespace
 
 extern "C" long long qt_cp_step_ws_bytes(void) { return (long long)WS_BYTES; }
@@ -886,7 +951,7 @@ extern "C" int qt_cp_step_supported(int H_, int I_, int Hq, int Hkv, int D_, int
          V / 16 <= NB && cp_step_resident();
 }
 
-extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
+static int qt_cp_step_check(const qt_cp_step_args* a) {
   if (!a || a->R < 1 || a->R > MAXR || a->n_layers < 1 || a->n_layers > 6) return QT_ERR_SHAPE;
   if (a->const_pos < 1 || a->const_pos > IC * GPW || a->const_pos >= a->Lmax) return QT_ERR_SHAPE;
   if (a->V % 16 || a->V / 16 > NB || a->V <= 0) return QT_ERR_SHAPE;
@@ -899,14 +964,42 @@ extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
         !a->k_cache[l] || !a->v_cache[l])
       return QT_ERR_ARG;
   if (!cp_step_resident()) return QT_ERR_SHAPE;
+  return 0;
+}
+
+extern "C" int qt_cp_step(const qt_cp_step_args* a, void* stream) {
+  const int rc = qt_cp_step_check(a);
+  if (rc) return rc;
   static const int spin = std::max(1000, qt_knob("QT_CE_SPIN", 200000));
   static const int lm = qt_knob("QT_CE_LM", 1);  // load timing (probe builds only: the product reads no env)
   const CEP pk{*a, spin};
-  if (lm == 0) hipLaunchKernelGGL((cp_step_k<0, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
-  else if (lm == 1) hipLaunchKernelGGL((cp_step_k<1, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
-  else hipLaunchKernelGGL((cp_step_k<2, 0>), dim3(NB), dim3(NT), 0, (hipStream_t)stream, pk);
-  return hipGetLastError() == hipSuccess ? 0 : QT_ERR_LAUNCH;
+  return cp_step_go(pk, lm, stream);
 }
+
+// qt_cp_step with the previous step's token choice at its start (qt_cp_step_sampled, include/qwen3tts_amd.h)
+extern "C" int qt_cp_step_sampled(const qt_cp_step_args* a, const qt_sample_args* sa, void* stream) {
+  if (!a || !sa || sa->R != a->R || sa->V <= 0 || sa->V > 2048 || !sa->tok_out || !sa->logits) return QT_ERR_SHAPE;
+  if (sa->do_sample && sa->top_k > sa->V) return QT_ERR_ARG;
+  if (sa->ctr_stride < 0 || (sa->force && (!sa->pick || !sa->codes))) return QT_ERR_ARG;
+  if (!sa->emb_table || sa->emb_dim != H || !sa->emb2_table || sa->emb2_dim != (NQ + 2 * NKV) * D) return QT_ERR_SHAPE;
+  qt_cp_step_args b = *a;  // qkv0 / x come from the sampler's rows: any non-null pointer passes the checks
+  if (!b.qkv0) b.qkv0 = sa->emb2_table;
+  if (!b.x) b.x = (float*)sa->emb_table;
+  const int rc = qt_cp_step_check(&b);
+  if (rc) return rc;
+  static const int spin = std::max(1000, qt_knob("QT_CE_SPIN", 200000));
+  static const int lm = qt_knob("QT_CE_LM", 1);
+  CEP pk{b, spin};
+  pk.fuse = 1;
+  pk.sa = *sa;
+  pk.sa.emb_table = nullptr;  // the engine gathers the rows itself
+  pk.sa.emb2_table = nullptr;
+  pk.sa.emb_out16 = nullptr;
+  pk.gx = sa->emb_table;
+  pk.gq = sa->emb2_table;
+  return cp_step_go(pk, lm, stream);
+}
+
 
 // The 2-token prefill of the same code predictor (M:1671-1675: positions 0 and 1 of every batch row -- the talker's
 // hidden state and its first code's embedding -- through all layers, their keys / values appended at cache positions 0

@@ -20,6 +20,7 @@ QT_DEV uint2 bld2_c(rsrc_t r, unsigned off) {
   return uint2{v[0], v[1]};
 }
 QT_DEV void bst_c(unsigned v, rsrc_t r, unsigned off) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, SC1); }
+QT_DEV void bst4_c(u32x4_t v, rsrc_t r, unsigned off) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, SC1); }
 QT_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 QT_DEV unsigned ld_flag(const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 QT_DEV void st_flag(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }

@@ -115,7 +115,7 @@ class SampleArgs(ctypes.Structure):
 EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decode_attention", "qt_decode_attn_ws_bytes",
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
-           "qt_cp_step", "qt_cp_prefill", "qt_cp_step_ws_bytes", "qt_cp_step_supported", "qt_cp_step_dbg_bytes",
+           "qt_cp_step", "qt_cp_prefill", "qt_cp_step_sampled", "qt_cp_step_ws_bytes", "qt_cp_step_supported", "qt_cp_step_dbg_bytes",
            "qt_talker_tail", "qt_talker_tail_ws_bytes", "qt_talker_tail_stamp_bytes", "qt_talker_tail_supported",
            "qt_talker_step", "qt_talker_step_ws_bytes", "qt_talker_step_stamp_bytes", "qt_talker_step_supported",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
@@ -177,7 +177,7 @@ def load_library(path: str = LIB_PATH):
         "qt_decode_attn_oproj": [P, P],
         "qt_attn_oproj_ws_bytes": [c_int, c_int],
         "qt_attn_oproj_resident_blocks": [],
-        "qt_cp_step": [P, P], "qt_cp_prefill": [P, P], "qt_cp_step_ws_bytes": [], "qt_cp_step_dbg_bytes": [],
+        "qt_cp_step": [P, P], "qt_cp_prefill": [P, P], "qt_cp_step_sampled": [P, P, P], "qt_cp_step_ws_bytes": [], "qt_cp_step_dbg_bytes": [],
         "qt_cp_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
         "qt_talker_tail": [P, P], "qt_talker_tail_ws_bytes": [], "qt_talker_tail_stamp_bytes": [],
         "qt_talker_tail_supported": [c_int, c_int, c_int, c_int, c_int],

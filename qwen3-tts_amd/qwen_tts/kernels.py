@@ -286,11 +286,13 @@ def cp_step_supported(H, I, Hq, Hkv, D, n_layers, V) -> bool:
     return bool(_hip.lib().qt_cp_step_supported(H, I, Hq, Hkv, D, n_layers, V))
 
 
-def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, sin, eps, logits, ws):
+def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, sin, eps, logits, ws, sample=None):
     """qt_cp_step: one code-predictor decode step (every layer + final norm + lm_head) in one persistent launch.
     layers: the code predictor's _Layer objects (tiled qkv / o / gate-up / down, q_norm / k_norm); kcs / vcs: per-layer
     bf16 caches [R][Hkv][Lmax][D]; x fp32 [R][H] input rows; qkv0 fp32 [R][qkv] layer-0 q/k/v rows; logits fp32 [R][V].
-    ws: zeroed uint8 scratch of cp_step_ws_bytes() kept across launches (word 0: the sticky hand-off error flag)."""
+    ws: zeroed uint8 scratch of cp_step_ws_bytes() kept across launches (word 0: the sticky hand-off error flag).
+    sample: qt_sample_args (sample(..., launch=False), with emb and emb2 tables) of the PREVIOUS step's token choice:
+    qt_cp_step_sampled runs it at the start of this launch and takes x / q/k/v from the chosen tokens' table rows."""
     a = _hip.CpStepArgs()
     a.R, a.n_layers, a.Lmax, a.const_pos, a.V, a.eps = R, len(layers), Lmax, const_pos, w_lm.N, eps
     a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
@@ -303,6 +305,9 @@ def cp_step(layers, w_lm: "Tiled", x, qkv0, R, kcs, vcs, Lmax, const_pos, cos, s
     a.qkv0, a.ldq = ptr(qkv0), qkv0.stride(0)
     a.logits, a.ldl = ptr(logits), logits.stride(0)
     a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    if sample is not None:
+        check(_hip.lib().qt_cp_step_sampled(ctypes.byref(a), ctypes.byref(sample), stream()), "qt_cp_step_sampled")
+        return
     check(_hip.lib().qt_cp_step(ctypes.byref(a), stream()), "qt_cp_step")
 
 
@@ -392,8 +397,9 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
            suppress=(0, 0, -1), ignore_eos=False, finished=None, do_sample=False, top_k=0, top_p=1.0,
            temperature=1.0, seed=0, step=None, substep=0, codes=None, codes_ld=0, codes_w=16, codes_col=0,
            codes_step_off=0, row_base=0, emb=None, seed_ptr=None, debug_u=-1.0, emb16=None, emb2=None, algo=0,
-           ctr_stride=0, philox_row=None, force=None, pick=None):
-    """step / n_generated: device int32 counters, one per row when ctr_stride = 1 (0: shared); philox_row: optional
+           ctr_stride=0, philox_row=None, force=None, pick=None, launch=True):
+    """launch=False: return the qt_sample_args instead (for qt_cp_step_sampled).
+    step / n_generated: device int32 counters, one per row when ctr_stride = 1 (0: shared); philox_row: optional
     device int32 [R] Philox stream ids (default row_base + r).
     force / pick (teacher forcing, parity diagnostics): int32 buffers in the layout of `codes`; the choice is stored
     in pick and the row continues with force's token.
@@ -419,6 +425,8 @@ def sample(logits, R, V, ld, tok_out, *, seen=None, rep_penalty=1.0, n_generated
             a.emb_out16, a.emb_ld16 = ptr(emb16[0]), emb16[1]
         if emb2 is not None:
             a.emb2_table, a.emb2_dim, a.emb2_out, a.emb2_ld = ptr(emb2[0]), emb2[0].shape[1], ptr(emb2[1]), emb2[2]
+    if not launch:
+        return a
     check(_hip.lib().qt_sample(ctypes.byref(a), stream()), "qt_sample")
 
 

@@ -146,6 +146,10 @@ CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
 # ... and the per-frame 2-token prefill through the same engine (qt_cp_prefill: 16 token rows, one launch instead of
 # ~26); QT_CP_PREFILL=0 keeps the launch chain for the prefill (A/B)
 CP_PREFILL = os.environ.get("QT_CP_PREFILL", "1") == "1"
+# ... and each step's token choice at the start of the NEXT step's launch (qt_cp_step_sampled: qt_sample's body on 4
+# waves of 8 workgroups, the chosen rows handed to the rest in-launch) instead of its own launch; QT_CP_FUSE_SAMPLE=0
+# keeps the qt_sample launches (A/B)
+CP_FUSE_SAMPLE = os.environ.get("QT_CP_FUSE_SAMPLE", "1") == "1"
 # talker decode layers: o_proj -> gate/up -> down -> next layer's q/k/v as ONE persistent launch per layer (qt_talker_tail:
 # weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
 # four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
@@ -637,10 +641,15 @@ class TalkerEngine:
             ln.x.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
             if ln.x16 is not None:
                 ln.x16.view(nb, 2, Hc)[:, 0].copy_(s.past_hidden[ln.b0:ln.b1])
+        fuse = ln.ce_ws is not None and CP_FUSE_SAMPLE and self.Vc <= 2048
+        pending = None  # the token choice the next step's launch makes first (fused)
         if ln.ce_ws is not None and CP_PREFILL:  # every layer + lm_head[0] for both positions in one launch
             K.cp_prefill(c.layers, self.lm_heads[0], ln.x, nb, ln.kv[0], ln.kv[1], s.cp_L, c.cos, c.sin, c.eps,
                          ln.logits, ln.ce_ws)
-            self._cp_sample(s, ln, 0)
+            if fuse:
+                pending = self._cp_sample(s, ln, 0, launch=False)
+            else:
+                self._cp_sample(s, ln, 0)
         else:
             p16 = ln.x16 if 2 * nb <= 96 else None  # forward() keeps the shadow for decode / skinny-GEMV row counts
             c.forward(ln.x, 2 * nb, ln.meta0, ln.kv, ln.sc, s.cp_L, s.cp_L, x16=p16)
@@ -650,8 +659,12 @@ class TalkerEngine:
             x16 = None if ln.x16 is None else ln.x16[:nb]
             if ln.ce_ws is not None:  # the whole step (5 layers + lm_head[g]) in one persistent launch
                 K.cp_step(c.layers, self.lm_heads[g], x, ln.sc["qkv"][:nb], nb, ln.kv[0], ln.kv[1], s.cp_L, g + 1,
-                          c.cos, c.sin, c.eps, ln.logits, ln.ce_ws)
-                self._cp_sample(s, ln, g)
+                          c.cos, c.sin, c.eps, ln.logits, ln.ce_ws, sample=pending)
+                if fuse and g < self.G - 2:
+                    pending = self._cp_sample(s, ln, g, launch=False)
+                else:
+                    pending = None
+                    self._cp_sample(s, ln, g)
                 continue
             c.forward(x, nb, ln.meta[g - 1], ln.kv, ln.sc, s.cp_L, s.cp_L, decode=True, x16=x16,
                       qkv0=self.cp_qkv_tabs is not None)
@@ -662,9 +675,9 @@ class TalkerEngine:
         K.gemm(h if h16 is None else h16, self.lm_heads[g], ln.logits, ln.nb, ldh, self.Vc, rms=True, eps=c.eps)
         self._cp_sample(s, ln, g)
 
-    def _cp_sample(self, s: Session, ln: CPLane, g):
+    def _cp_sample(self, s: Session, ln: CPLane, g, launch=True):
         c, gp = self.cp, s.gp
-        K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
+        return K.sample(ln.logits, ln.nb, self.Vc, self.Vc, ln.tok, do_sample=gp.subtalker_dosample,
                  top_k=gp.subtalker_top_k, top_p=gp.subtalker_top_p, temperature=gp.subtalker_temperature,
                  seed_ptr=s.seed, step=s.step[ln.b0:ln.b1], substep=1 + g, codes=ln.codes,
                  codes_ld=s.codes.shape[1] * self.G, codes_w=self.G, codes_col=1 + g, codes_step_off=0, ctr_stride=1,
@@ -674,7 +687,7 @@ class TalkerEngine:
                  emb2=(self.cp_qkv_tabs[g], ln.sc["qkv"], c.qkv_w) if self.cp_qkv_tabs is not None and g < self.G - 2
                  else None,
                  force=None if s.force is None else s.force[ln.b0:ln.b1],
-                 pick=None if s.pick is None else s.pick[ln.b0:ln.b1])
+                 pick=None if s.pick is None else s.pick[ln.b0:ln.b1], launch=launch)
 
     # ---------------------------------------------------------------- G2/G3: prefill + decode loop
     def generate_from_embeds(self, embeds: torch.Tensor, mask: torch.Tensor, trailing: torch.Tensor,

@@ -195,3 +195,53 @@ def test_cp_prefill_matches_launch_chain(R):
         assert torch.equal(kc2[li][:, :, 2:], kc1[li][:, :, 2:])  # nothing else written
         assert torch.equal(vc2[li][:, :, 2:], vc1[li][:, :, 2:])
     assert int(ws[4:8].view(torch.int32).item()) == 4  # 3 prefills + 1 decode step advanced the launch counter
+
+
+@pytest.mark.parametrize("R,do_sample,force", [(8, True, False), (5, True, True), (3, False, False)])
+def test_cp_step_sampled_equals_sample_then_step(R, do_sample, force):
+    """qt_cp_step_sampled (the previous step's qt_sample body run inside the engine launch, the chosen rows handed over
+    in-launch) against qt_sample followed by qt_cp_step on the same logits / tables / counters: the same tokens, codes
+    and teacher-forcing picks, and bit-identical logits and appended K/V (the engine sees the same input rows)."""
+    from qwen_tts import kernels as Kn
+    dev = _dev()
+    st, lm, g = _cp_stack(dev, seed=7)
+    if not Kn.cp_step_supported(st.H, st.I, st.Hq, st.Hkv, st.D, st.n_layers, lm.N):
+        pytest.skip("qt_cp_step not supported on this device")
+    Lmax, V, pos, G = 18, lm.N, 6, 16
+    prev_logits = (torch.randn(R, V, generator=g) * 3).to(dev)
+    tab_x = torch.randn(V, st.H, generator=g).to(dev)
+    tab_q = torch.randn(V, st.qkv_w, generator=g).to(dev)
+    kc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    vc = [torch.randn(R, st.Hkv, Lmax, st.D, generator=g).to(dev, torch.bfloat16) for _ in st.layers]
+    step = torch.tensor([3, 1, 4, 1, 5, 9, 2, 6][:R], dtype=torch.int32, device=dev)
+    prow = torch.arange(10, 10 + R, dtype=torch.int32, device=dev)
+    seed = torch.tensor([1234567], dtype=torch.int64, device=dev)
+    frc = torch.randint(0, V, (R, 12 * G), generator=g, dtype=torch.int32).to(dev) if force else None
+
+    def run(fused):
+        codes = torch.full((R, 12 * G), -1, dtype=torch.int32, device=dev)
+        pick = torch.full((R, 12 * G), -1, dtype=torch.int32, device=dev) if force else None
+        tok = torch.full((R,), -1, dtype=torch.int32, device=dev)
+        x = torch.zeros(R, st.H, device=dev)
+        q0 = torch.zeros(R, st.qkv_w, device=dev)
+        k2, v2 = [k.clone() for k in kc], [v.clone() for v in vc]
+        logits = torch.full((R, V), float("nan"), device=dev)
+        ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
+        sa = Kn.sample(prev_logits, R, V, V, tok, do_sample=do_sample, top_k=50, top_p=1.0, temperature=0.9,
+                       seed_ptr=seed, step=step, substep=pos, codes=codes, codes_ld=12 * G, codes_w=G,
+                       codes_col=pos - 1, codes_step_off=0, ctr_stride=1, philox_row=prow, emb=(tab_x, x, st.H),
+                       emb2=(tab_q, q0, st.qkv_w), force=frc, pick=pick, launch=not fused)
+        Kn.cp_step(st.layers, lm, x, q0, R, k2, v2, Lmax, pos, st.cos, st.sin, st.eps, logits, ws,
+                   sample=sa if fused else None)
+        torch.cuda.synchronize()
+        assert int(ws[:4].view(torch.int32).item()) == 0, "hand-off poll gave up"
+        return tok, codes, pick, logits, k2, v2
+
+    ref, fus = run(False), run(True)
+    print(f"\n  R={R} sample={do_sample} force={force}: tokens {ref[0].tolist()} / {fus[0].tolist()}")
+    assert torch.equal(ref[0], fus[0]) and torch.equal(ref[1], fus[1])
+    if force:
+        assert torch.equal(ref[2], fus[2])
+    assert torch.equal(ref[3], fus[3])
+    for a, b in zip(ref[4] + ref[5], fus[4] + fus[5]):
+        assert torch.equal(a, b)
