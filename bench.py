@@ -166,10 +166,23 @@ def cp_step_entry(tts, B, Lmax=18, reps=20):
     logits = torch.empty(B, eng.Vc, device=dev)
     ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
     steps = list(range(1, eng.G - 1))
+    from qwen_tts.talker import CP_FUSE_SAMPLE
+    fuse = CP_FUSE_SAMPLE and eng.cp_in_tabs is not None and eng.cp_qkv_tabs is not None
+    if fuse:  # each launch first makes the previous step's token choice (qt_cp_step_sampled), as in a frame
+        logits.normal_()
+        i32 = lambda v: torch.full((B,), v, dtype=torch.int32, device=dev)  # noqa: E731
+        tok, stp, prow = i32(0), i32(0), torch.arange(B, dtype=torch.int32, device=dev)
+        seed = torch.tensor([7], dtype=torch.int64, device=dev)
+        codes = torch.zeros(B, 4 * eng.G, dtype=torch.int32, device=dev)
+        sas = [Kn.sample(logits, B, eng.Vc, eng.Vc, tok, do_sample=True, top_k=50, top_p=1.0, temperature=0.9,
+                         seed_ptr=seed, step=stp, substep=g, codes=codes, codes_ld=4 * eng.G, codes_w=eng.G,
+                         codes_col=g, ctr_stride=1, philox_row=prow, emb=(eng.cp_in_tabs[g - 1], x, c.H),
+                         emb2=(eng.cp_qkv_tabs[g - 1], qkv, c.qkv_w), launch=False) for g in steps]
 
     def run():
-        for g in steps:
-            Kn.cp_step(c.layers, eng.lm_heads[g], x, qkv, B, kc, vc, Lmax, g + 1, c.cos, c.sin, c.eps, logits, ws)
+        for i, g in enumerate(steps):
+            Kn.cp_step(c.layers, eng.lm_heads[g], x, qkv, B, kc, vc, Lmax, g + 1, c.cos, c.sin, c.eps, logits, ws,
+                       sample=sas[i] if fuse else None)
     us = _graph_us(run, dev, reps) / len(steps)
     assert int(ws[:4].view(torch.int32).item()) == 0, "cp_step hand-off flag set during the kernel-table run"
     L0 = c.layers[0]
@@ -178,8 +191,11 @@ def cp_step_entry(tts, B, Lmax=18, reps=20):
     el = kc[0].element_size()
     kv = sum(len(c.layers) * B * c.Hkv * c.D * el * (2 * (g + 1) + 2) for g in steps) / len(steps)
     byt = int(wb + lm + kv + B * (c.H + c.qkv_w + eng.Vc) * 4)
+    if fuse:  # + the sampled logits rows and the two gathered table rows
+        byt += B * (eng.Vc + c.H + c.qkv_w) * 4
     return dict(name="cp_step", kernel="cp_step_k (code-predictor step engine: 5 layers + lm_head in one launch, "
-                "keys 2..15)", bound="hbm", launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
+                "keys 2..15" + (", the previous step's token choice first" if fuse else "") + ")", bound="hbm",
+                launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
 
 
 def cp_prefill_entry(tts, B, Lmax=18, reps=20):

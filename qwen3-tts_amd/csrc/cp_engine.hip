@@ -65,12 +65,11 @@ struct Lay {
   static constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;                // NREPL replicas
   static constexpr size_t WS = OFF_H + NREPL * REPL_H;
 };
-// the fused sampler's hand-off (qt_cp_step_sampled): per-row flags, the chosen tokens' x rows and layer-0 q/k/v rows
-constexpr size_t OFF_SFL = Lay<16>::WS;                     // [8] flags (256 B)
-constexpr size_t OFF_SX = OFF_SFL + 256;                    // [8][H] fp32
-constexpr size_t OFF_SQ = OFF_SX + (size_t)8 * H * 4;       // [8][(NQ + 2 NKV) D] fp32
+// the fused sampler's hand-off (qt_cp_step_sampled): per row one {token, tag} granule; the consumers read the chosen
+// token's rows of the (read-only) tables themselves
+constexpr size_t OFF_SG = Lay<16>::WS;                      // [8] u64 granules (256 B reserved)
 constexpr int E_SAMP = 30;                                  // its tag slot
-constexpr size_t WS_BYTES = OFF_SQ + (size_t)8 * (NQ + 2 * NKV) * D * 4;
+constexpr size_t WS_BYTES = OFF_SG + 256;
 // optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
 // fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
 constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
@@ -132,7 +131,7 @@ struct Lds {
     bf16_t ha[MR / 4][HLD]; // the owner's SwiGLU rows, the A operand of down
     qt_sample_dev::SampSh samp;  // the fused sampler (layer 0, before any x16 staging)
   } a;
-  unsigned sb_cnt, sb_gen;  // the fused sampler's 4-wave barrier
+  unsigned sb_st[2];  // the fused sampler's barrier k: sb_st[k % 2] = 1 if it is the last (written before it)
   float red[NW][64][4];                                        // per-wave MFMA partials
   float rs[MR];                                                // 1 / rms per row
   float xown[MR / 4][16];                                      // the owned residual slices
@@ -293,8 +292,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       const int rr = orow(tid >> 4);
       s.xown[tid >> 4][tid & 15] = rr < RT && !fuse ? p.x[(long long)rr * p.ldx + 16 * to + (tid & 15)] : 0.f;
     } else if (tid == 144) {
-      s.sb_cnt = 0u;
-      s.sb_gen = 0u;
+      s.sb_st[0] = 0u;
+      s.sb_st[1] = 0u;
     } else if (tid >= 128 && tid < 144) {
       ((unsigned*)s.zero)[tid - 128] = 0u;
     } else if (tid >= 64 && tid < 128) {
@@ -385,29 +384,39 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   };
 
   const int L = p.n_layers;
+  // the fused sampler of row r = b / 33 (one workgroup per XCD) runs on its waves 0-3: qt_sample's body on the
+  // previous launch's logits (visible: kernel boundary); the chosen token goes out as the row's {token, tag} granule.
+  // Its barriers are block barriers: waves 4-7 pass barriers in a loop until the last one, which the sampler marks
+  // in a double-buffered LDS word before it (slot k % 2 is not rewritten before every wave has passed barrier k + 1).
+  // The sampler waves issue their own P2 loads only at the body's first barrier, after its logits loads (vmcnt
+  // retires in order).
+  u64* sgr = (u64*)(ws + OFF_SG);
+  const bool samp_blk = fuse && b % 33 == 0 && b / 33 < R;
   if constexpr (PF) load_p1(lp(PT_QKV, 0), (unsigned)(NQ + 2 * NKV) * D * H * 2, t1, threadIdx.x);
-  else load_p2(0, threadIdx.x);
-  const unsigned* sfl = (const unsigned*)(ws + OFF_SFL);
-  if (fuse && b % 33 == 0 && b / 33 < R && threadIdx.x < 256) {
-    // the fused sampler of row r = b / 33 (one block per XCD), waves 0-3: qt_sample's body on the previous launch's
-    // logits (visible: kernel boundary), then the chosen token's x row and layer-0 q/k/v row to the hand-off area
-    // (write-through), drained, then the row's flag
-    const int r = b / 33, tid = threadIdx.x;
-    CBar cb{&s.sb_cnt, &s.sb_gen};
-    unsigned g = 0;
-    const int tok = qt_sample_dev::sample_row<8>(pk.sa, 0, r, tid, s.a.samp, [&]() { cons_sync<4>(cb, g, pk.spin, err); });
-    const rsrc_t tx = mkr(pk.gx + (long long)tok * H, H * 4);
-    const rsrc_t tq = mkr(pk.gq + (long long)tok * (NQ + 2 * NKV) * D, (NQ + 2 * NKV) * D * 4);
-    const u32x4_t vx = bld(tx, tid * 16);
-    u32x4_t vq[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) vq[k] = bld(tq, (tid + 256 * k) * 16);
-    bst4_c(vx, wsr, (unsigned)(OFF_SX + (size_t)r * H * 4) + tid * 16);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) bst4_c(vq[k], wsr, (unsigned)(OFF_SQ + (size_t)r * (NQ + 2 * NKV) * D * 4) + (tid + 256 * k) * 16);
-    drain_stores();
-    cons_sync<4>(cb, g, pk.spin, err);
-    if (tid == 0) st_flag((unsigned*)sfl + r, tagof(E_SAMP));
+  else if (!(samp_blk && threadIdx.x < 256)) load_p2(0, threadIdx.x);
+  if (samp_blk) {
+    if (threadIdx.x < 256) {
+      const int r = b / 33, tid = threadIdx.x;
+      bool issued = false;
+      int kb = 0;
+      const int tok = qt_sample_dev::sample_row<8>(pk.sa, 0, r, tid, s.a.samp, [&]() {
+        if (!issued) { issued = true; load_p2(0, tid); }
+        if (tid == 0) s.sb_st[kb & 1] = 0u;
+        ++kb;
+        __syncthreads();
+      });
+      if (!issued) load_p2(0, tid);
+      if (tid == 0) {
+        st_g(sgr + r, (unsigned)tok, tagof(E_SAMP));
+        s.sb_st[kb & 1] = 1u;
+      }
+      __syncthreads();
+    } else {
+      for (int k = 0;; ++k) {
+        __syncthreads();
+        if (s.sb_st[k & 1]) break;
+      }
+    }
   }
   for (int l = 0; l < L; ++l) {
     // per-lane coordinates from an opaque thread id: derived values are recomputed per layer, not kept alive
@@ -478,16 +487,16 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       float xv[8];
       if (l == 0) {
         const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
-        if (fuse) {  // row r's q/k/v from the fused sampler's hand-off
+        if (fuse) {  // row r's q/k/v: the chosen token's row of the q/k/v table
           const unsigned want = tagof(E_SAMP);
-          for (int spins = 0; __builtin_amdgcn_readfirstlane(ld_flag(sfl + r)) != want; ++spins) {
+          u64 gv = ld_g(sgr + r);
+          for (int spins = 0; (unsigned)(__builtin_amdgcn_readfirstlane((unsigned)(gv >> 32))) != want; ++spins) {
             if (spins > pk.spin) { if (lane == 0) atomicOr(err, 1); break; }
             __builtin_amdgcn_s_sleep(1);
+            gv = ld_g(sgr + r);
           }
-          const unsigned o = (unsigned)OFF_SQ + (unsigned)(r * (NQ + 2 * NKV) * D + hh * D + e0) * 4;
-          const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
+          const int tok = min((int)(unsigned)gv, pk.sa.V - 1);
+          load8f(pk.gq + (long long)tok * (NQ + 2 * NKV) * D + (long long)hh * D + e0, xv);
         } else {
           load8f(p.qkv0 + (long long)r * p.ldq + (long long)hh * D + e0, xv);
         }
@@ -738,11 +747,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           float v = 0.f;
 #pragma unroll
           for (int hp = 0; hp < NKV; ++hp) v += s.gath[lane >> 5][hp][lane & 31];  // head order
-          if (fuse && l == 0) {  // the residual rows: the chosen tokens' x rows (every row's flag was seen in P2)
+          if (fuse && l == 0) {  // the residual rows: the chosen tokens' x rows (every row's granule was seen in P2)
             const int rr = orow(lane >> 4);
-            if (rr < RT)
-              s.xown[lane >> 4][lane & 15] =
-                  __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wsr, (int)(OFF_SX + ((size_t)rr * H + 16 * to + (lane & 15)) * 4), 0, SC1));
+            if (rr < RT) {
+              const int tok = min((int)(unsigned)ld_g(sgr + rr), pk.sa.V - 1);
+              s.xown[lane >> 4][lane & 15] = pk.gx[(long long)tok * H + 16 * to + (lane & 15)];
+            }
           }
           s.xown[lane >> 4][lane & 15] += v;
           if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
