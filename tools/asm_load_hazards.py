@@ -54,7 +54,9 @@ def check(body):
         args = line[len(op):].split(";")[0]
         if is_vmem:
             touched = regs(args)
-            if "load" in op or "atomic" in op and "glc" in args:
+            if "_lds_" in op:  # LDS-DMA (global_load_lds_*): the VGPR operand is the address, the data goes to LDS
+                dst, src = set(), touched
+            elif "load" in op or "atomic" in op and "glc" in args:
                 dst = regs(args.split(",")[0])
                 src = touched - dst
             else:
