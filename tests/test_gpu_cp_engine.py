@@ -197,11 +197,15 @@ def test_cp_prefill_matches_launch_chain(R):
     assert int(ws[4:8].view(torch.int32).item()) == 4  # 3 prefills + 1 decode step advanced the launch counter
 
 
-@pytest.mark.parametrize("R,do_sample,force", [(8, True, False), (5, True, True), (3, False, False)])
-def test_cp_step_sampled_equals_sample_then_step(R, do_sample, force):
+@pytest.mark.parametrize("R,do_sample,force,top_k,top_p", [(8, True, False, 50, 1.0), (5, True, True, 50, 1.0),
+                                                            (3, False, False, 50, 1.0), (8, True, False, 200, 0.8),
+                                                            (4, True, False, 0, 1.0)])
+def test_cp_step_sampled_equals_sample_then_step(R, do_sample, force, top_k, top_p):
     """qt_cp_step_sampled (the previous step's qt_sample body run inside the engine launch, the chosen rows handed over
     in-launch) against qt_sample followed by qt_cp_step on the same logits / tables / counters: the same tokens, codes
-    and teacher-forcing picks, and bit-identical logits and appended K/V (the engine sees the same input rows)."""
+    and teacher-forcing picks, and bit-identical logits and appended K/V (the engine sees the same input rows).  The
+    sampler paths: top-k 50 (histogram / per-wave candidates + Gumbel-max), top-k 200 with top-p 0.8 (the sorted
+    nucleus cut in the engine's LDS), no top-k (inverse CDF over the whole vocabulary), greedy."""
     from qwen_tts import kernels as Kn
     dev = _dev()
     st, lm, g = _cp_stack(dev, seed=7)
@@ -227,7 +231,7 @@ def test_cp_step_sampled_equals_sample_then_step(R, do_sample, force):
         k2, v2 = [k.clone() for k in kc], [v.clone() for v in vc]
         logits = torch.full((R, V), float("nan"), device=dev)
         ws = torch.zeros(Kn.cp_step_ws_bytes(), dtype=torch.uint8, device=dev)
-        sa = Kn.sample(prev_logits, R, V, V, tok, do_sample=do_sample, top_k=50, top_p=1.0, temperature=0.9,
+        sa = Kn.sample(prev_logits, R, V, V, tok, do_sample=do_sample, top_k=top_k, top_p=top_p, temperature=0.9,
                        seed_ptr=seed, step=step, substep=pos, codes=codes, codes_ld=12 * G, codes_w=G,
                        codes_col=pos - 1, codes_step_off=0, ctr_stride=1, philox_row=prow, emb=(tab_x, x, st.H),
                        emb2=(tab_q, q0, st.qkv_w), force=frc, pick=pick, launch=not fused)
@@ -238,7 +242,8 @@ def test_cp_step_sampled_equals_sample_then_step(R, do_sample, force):
         return tok, codes, pick, logits, k2, v2
 
     ref, fus = run(False), run(True)
-    print(f"\n  R={R} sample={do_sample} force={force}: tokens {ref[0].tolist()} / {fus[0].tolist()}")
+    print(f"\n  R={R} sample={do_sample} force={force} top_k={top_k} top_p={top_p}: tokens {ref[0].tolist()} / "
+          f"{fus[0].tolist()}")
     assert torch.equal(ref[0], fus[0]) and torch.equal(ref[1], fus[1])
     if force:
         assert torch.equal(ref[2], fus[2])
