@@ -30,6 +30,11 @@ sys.path.insert(0, os.path.join(REPO, "qwen3-tts_amd"))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# Infinity Cache (256 MiB die-level L3): no spec rate in the guide; its measured read rate from a 38 MB table gathered
+# chip-wide (MI355X_MICROARCH.md, "Indexed rows: gather into LDS": 8.6 TB/s) is the second bound of kernels whose bytes
+# stay resident there between two uses (the code predictor's 157 MB of layer weights, re-read by the 15 forwards of a
+# frame with ~161 MB touched in between)
+IC_RATE_GBS = 8600.0
 MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 
 
@@ -89,10 +94,12 @@ def frame_bytes(cfg, B, L_talker):
         return H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I
     w_t = t["num_hidden_layers"] * layer_params(t) + t["vocab_size"] * t["hidden_size"]
     w_cp = c["num_hidden_layers"] * layer_params(c) + c["vocab_size"] * c["hidden_size"]
+    # the 14 decode steps never read layer 0's q/k/v weights: their rows come from the precomputed table (bf16 mode)
+    qkv0 = c["hidden_size"] * (c["num_attention_heads"] + 2 * c["num_key_value_heads"]) * c["head_dim"]
     s2m = t["hidden_size"] * c["hidden_size"] if t["hidden_size"] != c["hidden_size"] else 0
     kv_t = t["num_hidden_layers"] * 2 * t["num_key_value_heads"] * t["head_dim"] * 2 * L_talker
     kv_cp = sum(c["num_hidden_layers"] * 2 * c["num_key_value_heads"] * c["head_dim"] * 2 * j for j in range(2, 17))
-    return 2 * (w_t + 15 * w_cp + s2m) + B * (kv_t + kv_cp)
+    return 2 * (w_t + 15 * w_cp - 14 * qkv0 + s2m) + B * (kv_t + kv_cp)
 
 
 def _gemv_entry(name, kernel, n_frame, Ws, M, K, N, a_dtype, o_dtype, dev, rms=False, epi=None, reps=10,
@@ -153,9 +160,11 @@ def attn_oproj_entry(tts, B, pos=9, reps=20, n_frame=None):
 
 def cp_step_entry(tts, B, Lmax=18, reps=20):
     """The code-predictor step engine (cp_step_k: 5 layers + lm_head[g] in one persistent launch), the 14 decode steps
-    of a frame (cache positions 2..15, lm_head 1..14) captured in one graph.  Algorithmic bytes per launch = the 5
-    layers' weights + lm_head[g] + the K/V rows read (pos keys per layer) and the new key written + x, the layer-0
-    q/k/v rows and the logits."""
+    of a frame (cache positions 2..15, lm_head 1..14) captured in one graph.  Algorithmic bytes per launch = what the
+    kernel reads and writes: the weights of layers 1-4 and layer 0's o_proj / gate-up / down (layer 0's q/k/v rows
+    come from the table, its q/k/v weights are never read) + lm_head[g] + the K/V rows read (pos keys per layer) and
+    the new key written + the x and layer-0 q/k/v input rows + the logits written (+ the previous logits read by the
+    fused token choice)."""
     from qwen_tts import kernels as Kn
     eng = tts.model.engine
     c, dev = eng.cp, eng.dev
@@ -185,17 +194,18 @@ def cp_step_entry(tts, B, Lmax=18, reps=20):
                        sample=sas[i] if fuse else None)
     us = _graph_us(run, dev, reps) / len(steps)
     assert int(ws[:4].view(torch.int32).item()) == 0, "cp_step hand-off flag set during the kernel-table run"
-    L0 = c.layers[0]
-    wb = sum(W.w.numel() * W.w.element_size() for W in (L0.qkv, L0.o, L0.gu, L0.down)) * len(c.layers)
-    lm = eng.lm_heads[1].w.numel() * eng.lm_heads[1].w.element_size()
+    nb = lambda W: W.w.numel() * W.w.element_size()  # noqa: E731  (tiled bf16 weights, no padding at these dims)
+    wb = sum(nb(L.o) + nb(L.gu) + nb(L.down) + (nb(L.qkv) if i > 0 else 0) for i, L in enumerate(c.layers))
+    lm = nb(eng.lm_heads[1])
     el = kc[0].element_size()
     kv = sum(len(c.layers) * B * c.Hkv * c.D * el * (2 * (g + 1) + 2) for g in steps) / len(steps)
+    # x + layer-0 q/k/v input rows (the chosen tokens' table rows when fused) and the logits written
     byt = int(wb + lm + kv + B * (c.H + c.qkv_w + eng.Vc) * 4)
-    if fuse:  # + the sampled logits rows and the two gathered table rows
-        byt += B * (eng.Vc + c.H + c.qkv_w) * 4
+    if fuse:  # + the previous step's logits rows read by the token choice
+        byt += B * eng.Vc * 4
     return dict(name="cp_step", kernel="cp_step_k (code-predictor step engine: 5 layers + lm_head in one launch, "
                 "keys 2..15" + (", the previous step's token choice first" if fuse else "") + ")", bound="hbm",
-                launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step")
+                launches_per_frame=len(steps), avg_us=us, bytes=byt, pmc_tag="cp_step", ic_resident=True)
 
 
 def cp_prefill_entry(tts, B, Lmax=18, reps=20):
@@ -222,7 +232,7 @@ def cp_prefill_entry(tts, B, Lmax=18, reps=20):
     kv = len(c.layers) * B * c.Hkv * c.D * kc[0].element_size() * 4
     byt = int(wb + lm + kv + B * (2 * c.H + eng.Vc) * 4)
     return dict(name="cp_prefill", kernel="cp_step_k<1, 1> (code-predictor 2-token prefill through the step engine)",
-                bound="hbm", launches_per_frame=1, avg_us=us, bytes=byt)
+                bound="hbm", launches_per_frame=1, avg_us=us, bytes=byt, ic_resident=True)
 
 
 def talker_tail_entry(tts, B, reps=5):
@@ -317,12 +327,13 @@ def _pmc_traffic(tag):
     for f in pmcs:
         j = json.load(open(os.path.join(pdir, f)))
         if j.get("build_id") == _hip.BUILD_ID:
-            return j.get("hbm_bytes_per_launch"), f"profiles/{f} (this build, {j['build_id']})"
+            return j.get("hbm_bytes_per_launch"), f"profiles/{f} (this build, {j['build_id']})", \
+                j.get("l2_to_cu_read_bytes_64B_req")
     if pmcs:
         j = json.load(open(os.path.join(pdir, pmcs[0])))
         return j.get("hbm_bytes_per_launch"), (f"profiles/{pmcs[0]} (earlier build {j.get('build_id')}, not this "
-                                               f"library's {_hip.BUILD_ID})")
-    return None, None
+                                               f"library's {_hip.BUILD_ID})"), j.get("l2_to_cu_read_bytes_64B_req")
+    return None, None, None
 
 
 PMC_TAG = {"talker_gateup": "gateup", "cp_attn_oproj": "attn_oproj", "cp_step": "cp_step", "talker_tail": "talker_tail"}
@@ -683,15 +694,29 @@ def main():
 
         def as_roof(e):
             tag = e.get("pmc_tag", PMC_TAG.get(e["name"]))
-            traffic, tsrc = _pmc_traffic(tag) if tag else (None, None)
+            traffic, tsrc, l2cu = _pmc_traffic(tag) if tag else (None, None, None)
             rp_us, rp_src = _rocprof_avg(tag) if tag else (None, None)
-            return {"bound": e["bound"], "kernel": e["kernel"], "achieved": round(e["gbs"], 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(e["frac"], 4), "traffic": traffic, "traffic_source": tsrc,
-                    "avg_launch_us": round(e["avg_us"], 2), "bytes_per_launch": int(e["bytes"]),
-                    "launches_per_frame": e["launches_per_frame"], "us_per_frame": round(e["us_per_frame"], 1),
-                    "frame_share": None if frame_us is None else round(e["us_per_frame"] / frame_us, 4),
-                    "rocprof_avg_us": rp_us, "rocprof_source": rp_src,
-                    "achieved_at_rocprof_avg": None if not rp_us else round(e["bytes"] / (rp_us * 1e-6) / 1e9, 1)}
+            ach_rp = None if not rp_us else e["bytes"] / (rp_us * 1e-6) / 1e9
+            r = {"bound": e["bound"], "kernel": e["kernel"], "achieved": round(e["gbs"], 1), "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": round(e["frac"], 4), "traffic": traffic, "traffic_source": tsrc,
+                 "traffic_over_bytes": None if not traffic else round(traffic / e["bytes"], 3),
+                 "l2_to_cu_over_bytes": None if not l2cu else round(l2cu / e["bytes"], 3),
+                 "avg_launch_us": round(e["avg_us"], 2), "bytes_per_launch": int(e["bytes"]),
+                 "launches_per_frame": e["launches_per_frame"], "us_per_frame": round(e["us_per_frame"], 1),
+                 "frame_share": None if frame_us is None else round(e["us_per_frame"] / frame_us, 4),
+                 "rocprof_avg_us": rp_us, "rocprof_source": rp_src,
+                 "achieved_at_rocprof_avg": None if ach_rp is None else round(ach_rp, 1),
+                 "frac_at_rocprof_avg": None if ach_rp is None else round(ach_rp / HBM_PEAK_GBS, 4),
+                 "timing_note": "avg_launch_us: a graph of the frame's launches replayed between HIP events on their "
+                                "stream, divided by the launches (each dependent launch's dispatch gap included); "
+                                "rocprof_avg_us: the kernel's own begin -> end in rocprofv3 --kernel-trace"}
+            if e.get("ic_resident"):  # second bound: the weights are re-read from the Infinity Cache within a frame
+                r["second_bound"] = {"bound": "infinity_cache", "achieved": round(e["gbs"], 1), "peak": IC_RATE_GBS,
+                                     "unit": "GB/s", "frac": round(e["gbs"] / IC_RATE_GBS, 4),
+                                     "frac_at_rocprof_avg": None if ach_rp is None else round(ach_rp / IC_RATE_GBS, 4),
+                                     "peak_source": "MI355X_MICROARCH.md: measured chip-wide read rate from a 38 MB "
+                                                    "table in the Infinity Cache (no spec figure)"}
+            return r
         # the dominant decode kernel = the largest measured time per frame (launch time x launches per frame)
         dom = max(tab, key=lambda e: e["us_per_frame"])
         roof = dict(as_roof(dom), selected_by="largest measured time per frame among the decode kernels (kernel_table)")

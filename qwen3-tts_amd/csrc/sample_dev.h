@@ -1,7 +1,9 @@
 // Logits processing + token selection (transformers 4.57 semantics) for one row on 256 threads (4 waves): the body of
 // qt_sample's kernel (sample.hip), also run inside the code-predictor step engine (cp_engine.hip) by waves 0-3 of a
-// workgroup whose other waves do not take part -- hence the barrier is a parameter (__syncthreads in the kernel, an
-// LDS arrival counter of the 4 waves in the engine).  Method notes: sample.hip's header.
+// workgroup whose other waves do not take part -- hence the barrier is a parameter: __syncthreads in the kernel; in the
+// engine a block-wide __syncthreads too, which the non-sampling waves 4-7 pass in a loop until the sampler marks its
+// last barrier in the double-buffered LDS word sb_st (cp_engine.hip, the fused sampler block).  Method notes:
+// sample.hip's header.
 #pragma once
 #include "common.h"
 

@@ -121,7 +121,10 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
 #pragma unroll
           for (int c = 0; c < NWC; ++c) m = min(m, lds_ld(&s.done[c]));
           if ((int)__builtin_amdgcn_readfirstlane(m) >= sq - NSLOT + 1) break;
-          if (spins > pk.spin) { if (lane == 0) atomicOr(err, 2); break; }
+          // a full ring waits for the consumers, which may themselves sit in a hand-off poll of up to pk.spin x
+          // (global sc1 load + s_sleep 1): bounded like cons_sync (64 x spin LDS polls), not by pk.spin, so the loader
+          // never gives up (and overwrites a slot in use) before the consumers' own poll would
+          if (spins > 64 * pk.spin) { if (lane == 0) atomicOr(err, 2); break; }
           __builtin_amdgcn_s_sleep(0);
         }
       }

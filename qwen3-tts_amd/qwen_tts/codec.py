@@ -9,7 +9,6 @@ columns are already the time-interleaved samples: no pixel shuffle pass).
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, List
 
 import torch
@@ -271,7 +270,7 @@ class _StreamSlot:
 
 
 # captured feed graphs (per slot and feed shape, once a shape repeats); QT_CODEC_GRAPH=0 always feeds eagerly (A/B)
-CODEC_GRAPH = os.environ.get("QT_CODEC_GRAPH", "1") == "1"
+CODEC_GRAPH = _hip.lib_knob("QT_CODEC_GRAPH", 1) != 0
 
 
 class CodecStream:

@@ -329,46 +329,6 @@ def cp_prefill(layers, w_lm: "Tiled", x, R, kcs, vcs, Lmax, cos, sin, eps, logit
     check(_hip.lib().qt_cp_prefill(ctypes.byref(a), stream()), "qt_cp_prefill")
 
 
-def talker_step_ws_bytes():
-    return int(_hip.lib().qt_talker_step_ws_bytes())
-
-
-def talker_step_supported(H, I, Hq, Hkv, D, n_layers) -> bool:
-    return bool(_hip.lib().qt_talker_step_supported(H, I, Hq, Hkv, D, n_layers))
-
-
-def talker_step_table(layers, kcs, vcs, dev):
-    """The device pointer table qt_talker_step reads ([kind][layer]: q/k/v, o_proj, gate/up, down, q_norm, k_norm,
-    k_cache, v_cache); build once per (weights, caches)."""
-    cols = [[ptr(L.qkv.w) for L in layers], [ptr(L.o.w) for L in layers], [ptr(L.gu.w) for L in layers],
-            [ptr(L.down.w) for L in layers], [ptr(L.q_norm) for L in layers], [ptr(L.k_norm) for L in layers],
-            [ptr(k) for k in kcs], [ptr(v) for v in vcs]]
-    flat = [c or 0 for col in cols for c in col]
-    return torch.tensor(flat, dtype=torch.int64).to(dev)
-
-
-def talker_step(wtab, n_layers, R, x, Lmax, cos, sin, rope_pos, kv_pos, row_start, row_batch, eps, ws,
-                first_layer=0, total_layers=None, qkv_in=None, qkv_out=None, att_in=None, att_out=None):
-    """qt_talker_step: talker decoder layers [first_layer, first_layer + n_layers) of one decode step in one persistent
-    launch.  wtab from talker_step_table() (all layers); x fp32 [R][H] input rows, overwritten with the last layer's
-    output; the int32 row arrays as qt_decode_attention takes them.  qkv_in: the first layer's q/k/v rows (fp32
-    [R][4096], its projection skipped); qkv_out: also compute the next layer's q/k/v rows into it.  ws: zeroed uint8
-    scratch of talker_step_ws_bytes() kept across launches."""
-    a = _hip.TalkerStepArgs()
-    a.R, a.n_layers, a.Lmax, a.eps = R, n_layers, Lmax, eps
-    a.first_layer, a.total_layers = first_layer, n_layers if total_layers is None else total_layers
-    a.qkv_in, a.ldq_in = (ptr(qkv_in), qkv_in.stride(0)) if qkv_in is not None else (None, 0)
-    a.qkv_out, a.ldq_out = (ptr(qkv_out), qkv_out.stride(0)) if qkv_out is not None else (None, 0)
-    a.att_in, a.lda_in = (ptr(att_in), att_in.stride(0)) if att_in is not None else (None, 0)
-    a.att_out, a.lda_out = (ptr(att_out), att_out.stride(0)) if att_out is not None else (None, 0)
-    a.wtab = ptr(wtab)
-    a.cos_tab, a.sin_tab = ptr(cos), ptr(sin)
-    a.rope_pos, a.kv_pos, a.row_start, a.row_batch = ptr(rope_pos), ptr(kv_pos), ptr(row_start), ptr(row_batch)
-    a.x, a.ldx = ptr(x), x.stride(0)
-    a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
-    check(_hip.lib().qt_talker_step(ctypes.byref(a), stream()), "qt_talker_step")
-
-
 def talker_tail_ws_bytes():
     return int(_hip.lib().qt_talker_tail_ws_bytes())
 

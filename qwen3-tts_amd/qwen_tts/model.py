@@ -11,7 +11,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import kernels as K
-from .talker import MIN_NEW_TOKENS, GenParams, TalkerEngine
+from .talker import MIN_NEW_TOKENS, GenParams, HandoffWatch, TalkerEngine
 
 
 class _Runs:
@@ -533,7 +533,10 @@ class TTSModel:
                 # the EOS scan reads cb0 on the host (a sync on the frame just launched); columns [0, frames] hold
                 # tokens sampled at n_generated <= frames, and EOS is suppressed below MIN_NEW_TOKENS, so the first
                 # chunk skips the scan and its codec feed is queued right behind the frame
-                if final or frames + 1 > MIN_NEW_TOKENS:
+                # frames not covered by a watch check yet (the early first chunk skips the scan): checked, behind their
+                # codec feed, before the first of their audio is handed out
+                unchecked = not (final or frames + 1 > MIN_NEW_TOKENS)
+                if not unchecked:
                     c0 = codes[:, :, 0].cpu()
                     for b in range(B):
                         if end[b] is None:
@@ -575,6 +578,9 @@ class TTSModel:
                         o = ctx_s + emit_s + (lo_s - gpos)
                         chunk = cs.pcm[b, o:o + max(hi_s - lo_s, 0)]
                         done[b] = last
+                        if unchecked:  # flags copied behind the feed that produced this PCM: the caller waits on it anyway
+                            HandoffWatch(sessions).check()
+                            unchecked = False
                         yield b, chunk, last
                     emit_s += n
                     gpos += n
@@ -586,6 +592,9 @@ class TTSModel:
                 if t_end is not None and fed >= t_end:
                     for b in range(B):  # rows whose output was complete before the last window
                         if not done[b]:
+                            if unchecked:
+                                HandoffWatch(sessions).check()
+                                unchecked = False
                             done[b] = True
                             yield b, torch.zeros(0, device=codes.device), True
                 if all(done):

@@ -10,7 +10,6 @@ Per-request state lives in a `Session` object, never on the module (fixes the re
 """
 from __future__ import annotations
 
-import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -128,51 +127,44 @@ class _Stack:
 
 # code-predictor decode steps: qt_decode_attn_oproj (attention fused into o_proj + residual); QT_ATTN_OPROJ=0 keeps
 # the two-launch path (decode attention, then the o_proj GEMV) for A/B measurement
-ATTN_OPROJ = os.environ.get("QT_ATTN_OPROJ", "1") == "1"
+ATTN_OPROJ = _hip.lib_knob("QT_ATTN_OPROJ", 1) != 0
 # ... for lanes of at most this many rows: every block of the fused kernel re-reads its o_proj weight slice per row
 # (R x 4 MiB through L2 per launch), so at 64 rows it took 50.5 us per launch (bench --workload vd64 profile).
 # vd64 audio-s/s with 16 / 32 / 64 refilled rows: fused 238 / 285 / 328, two launches 254 / 337 / 452
 # (profiles/r03_attn_oproj_rows_ab.txt); at 8 rows the fused launch wins (round 2: 155.9 -> 164.0).  QT_ATTN_OPROJ_MAX
 # overrides (A/B)
-ATTN_OPROJ_MAX = _hip.env_int("QT_ATTN_OPROJ_MAX", 8)
+ATTN_OPROJ_MAX = _hip.lib_knob("QT_ATTN_OPROJ_MAX", 8)
 # ... in its head-split form (qt_attn_oproj_args.ws: per-(column group, kv head) blocks exchanging row partials): 2.5x
 # less L2 -> CU traffic than the (column group, row) form (profiles/r04_pmc_attn_oproj*.json), 7.71 -> 7.03 us per
 # launch, bench 200.2 -> 202.8 audio-s/s (profiles/r04_bench_ab_ao_hs.txt).  QT_AO_HS=0 keeps the other form (A/B)
-AO_HS = os.environ.get("QT_AO_HS", "1") == "1"
+AO_HS = _hip.lib_knob("QT_AO_HS", 1) != 0
 # code-predictor decode steps as ONE persistent launch each (qt_cp_step: every layer + lm_head, in-launch hand-offs)
 # instead of ~21 dependent launches (bf16 mode with the layer-0 q/k/v tables, <= 8 rows); QT_CP_ENGINE=0 keeps the
 # launch chain (A/B)
-CP_ENGINE = os.environ.get("QT_CP_ENGINE", "1") == "1"
+CP_ENGINE = _hip.lib_knob("QT_CP_ENGINE", 1) != 0
 # ... and the per-frame 2-token prefill through the same engine (qt_cp_prefill: 16 token rows, one launch instead of
 # ~26); QT_CP_PREFILL=0 keeps the launch chain for the prefill (A/B)
-CP_PREFILL = os.environ.get("QT_CP_PREFILL", "1") == "1"
+CP_PREFILL = _hip.lib_knob("QT_CP_PREFILL", 1) != 0
 # ... and each step's token choice at the start of the NEXT step's launch (qt_cp_step_sampled: qt_sample's body on 4
 # waves of 8 workgroups, the chosen rows handed to the rest in-launch) instead of its own launch; QT_CP_FUSE_SAMPLE=0
 # keeps the qt_sample launches (A/B)
-CP_FUSE_SAMPLE = os.environ.get("QT_CP_FUSE_SAMPLE", "1") == "1"
+CP_FUSE_SAMPLE = _hip.lib_knob("QT_CP_FUSE_SAMPLE", 1) != 0
 # talker decode layers: o_proj -> gate/up -> down -> next layer's q/k/v as ONE persistent launch per layer (qt_talker_tail:
 # weights streamed through an LDS ring by loader waves, in-launch hand-offs) after each layer's attention, instead of
 # four GEMV launches (bf16 mode, <= 8 rows, the 1.7B talker's shapes); QT_TALKER_TAIL=0 keeps the launch chain (A/B)
-TALKER_TAIL = os.environ.get("QT_TALKER_TAIL", "1") == "1"
-# ... or qt_talker_step (attention inside the weight-ring launch) when the frame's attention runs unsplit (A/B only):
-# QT_TALKER_STEP=1 every layer in ONE launch, 2 = one launch per layer (attention .. next q/k/v, the q/k/v rows crossing
-# the boundary).  Both measured slower than attention + qt_talker_tail (B = 8, 267 keys: 39.4 / 44.7 vs 36.6 us per
-# layer; a third form, o_proj .. the next layer's attention per launch, 48.9: profiles/r05_talker_step_ab.txt -- in-
-# launch hand-offs under the weight stream cost 2-5 us each, more than the kernel boundaries they replace), so 0 = off
-# is the default
-TALKER_STEP = _hip.env_int("QT_TALKER_STEP", 0)
+TALKER_TAIL = _hip.lib_knob("QT_TALKER_TAIL", 1) != 0
 # bf16 residual shadows as the RMS-normalised GEMVs' A operand (bf16 mode); QT_X16=0 reads the fp32 stream (A/B)
-X16 = os.environ.get("QT_X16", "1") == "1"
+X16 = _hip.lib_knob("QT_X16", 1) != 0
 # code-predictor layer-0 q/k/v rows gathered from precomputed tables (bf16 mode); QT_QKV0_TAB=0 keeps the GEMV (A/B)
-QKV0_TAB = os.environ.get("QT_QKV0_TAB", "1") == "1"
+QKV0_TAB = _hip.lib_knob("QT_QKV0_TAB", 1) != 0
 # talker prefill captured into a HIP graph per (session, prompt length) once that length repeats; QT_PREFILL_GRAPH=0
 # always issues it eagerly (A/B)
-PREFILL_GRAPH = os.environ.get("QT_PREFILL_GRAPH", "1") == "1"
+PREFILL_GRAPH = _hip.lib_knob("QT_PREFILL_GRAPH", 1) != 0
 # large-M prefill linears on gemm_pf_k (LDS-staged bf16 A and B): the prefill keeps the bf16 residual shadow at any
 # row count, so its RMS GEMMs read bf16 A too; QT_PF=0 (read by the library as well) keeps igemm_k (A/B)
 PF = _hip.lib_knob("QT_PF", 1) != 0  # as the library reads it (probe builds only)
 # static prefill buffers (+ captured graphs) kept per session: the most recently used prompt lengths, LRU-evicted
-PREFILL_CACHE = max(1, _hip.env_int("QT_PREFILL_CACHE", 4))
+PREFILL_CACHE = max(1, _hip.lib_knob("QT_PREFILL_CACHE", 4))
 # the generation config's min_new_tokens (M:2044-2066): EOS is suppressed while a row has generated fewer tokens
 MIN_NEW_TOKENS = 2
 # talker decode attention split-KV by cache length: (keys below which, nsplit).  B = 8, 1.7B (tools/talker_attn_bench.py,
@@ -180,7 +172,7 @@ MIN_NEW_TOKENS = 2
 # 14.4 / 15.1 / 21.0, 2048 26.9 / 20.3 / 20.3 / 25.8, 4000 47.2 / 31.9 / 30.4 / 36.0.  The frame graph is captured once
 # per split factor and the host picks the graph from its bound on the longest row's key count.  QT_ATTN_SPLIT=0 keeps
 # one block per (row, kv head) at every length (A/B)
-ATTN_SPLIT = [(768, 1), (2048, 2), (1 << 30, 4)] if _hip.env_int("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
+ATTN_SPLIT = [(768, 1), (2048, 2), (1 << 30, 4)] if _hip.lib_knob("QT_ATTN_SPLIT", 1) else [(1 << 30, 1)]
 
 
 def attn_nsplit(keys: int) -> int:
@@ -219,16 +211,28 @@ def _scratch(R, st: _Stack, dev, attn_oproj=False):
     return sc
 
 
-HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step / qt_talker_tail / "
-                 "qt_talker_step; blocks not co-resident?); outputs of this request are invalid (QT_AO_HS=0 / "
-                 "QT_CP_ENGINE=0 / QT_TALKER_TAIL=0 / QT_TALKER_STEP=0 select the forms without hand-offs)")
+HANDOFF_ERROR = ("an in-launch hand-off timed out (qt_decode_attn_oproj head-split / qt_cp_step / qt_talker_tail; "
+                 "blocks not co-resident?); outputs of this request are invalid (qwen_tts.talker.AO_HS / CP_ENGINE / "
+                 "TALKER_TAIL = False before the model is built select the forms without hand-offs)")
+
+
+class HandoffError(RuntimeError):
+    """A hand-off give-up during continuous batching (serve()): the session's flag word is sticky and session-wide, so
+    every request decoding when it was set is suspect.  The session stops cleanly: `failed` lists the request indices
+    that were in flight (their results are not handed out), `not_started` those still queued; requests yielded
+    before are unaffected (their frames were checked clear)."""
+
+    def __init__(self, failed, not_started):
+        super().__init__(HANDOFF_ERROR + f" [serve(): in-flight requests {sorted(failed)} failed, "
+                                         f"{len(not_started)} queued requests not started]")
+        self.failed, self.not_started = sorted(failed), list(not_started)
 
 
 def _flag_words(s):
-    """The sticky hand-off error words of a session's in-launch hand-off kernels (head-split attention + o_proj,
-    the code-predictor step engine), int32 device views."""
+    """The sticky hand-off error words of a session's in-launch hand-off kernels (head-split attention + o_proj, the
+    code-predictor step engine, the talker tail engine), int32 device views."""
     out = []
-    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws, s.sc_t.get("tt_ws"), getattr(s, "ts_ws", None)):
+    for ws in (s.cp.sc.get("ao_ws"), s.cp.ce_ws, s.sc_t.get("tt_ws")):
         if ws is not None:
             out.append(ws[:4].view(torch.int32))
     return out
@@ -407,12 +411,6 @@ class Session:
                                            device=dev)
         if eng.talker_tail and B <= 8:  # the talker decode-layer tail engine's hand-off workspace (zeroed once)
             self.sc_t["tt_ws"] = torch.zeros(K.talker_tail_ws_bytes(), dtype=torch.uint8, device=dev)
-        # the talker decode-step engine: its hand-off workspace and the pointer table of this session's caches
-        self.ts_ws = self.ts_tab = None
-        if eng.talker_step and B <= 8:
-            self.ts_ws = torch.zeros(K.talker_step_ws_bytes(), dtype=torch.uint8, device=dev)
-            self.ts_tab = K.talker_step_table(t.layers, self.kv[0], self.kv[1], dev)
-            self.ts_q = [f32(B, t.qkv_w), f32(B, t.qkv_w)]  # per-layer launches: q/k/v rows in / out
         self.codes = i32(B, max_frames + 2, self.G)
         # teacher forcing (parity diagnostics): every sampler continues with force[] and records its choice in pick[]
         self.force = i32(B, max_frames + 2, self.G) if teacher else None
@@ -490,8 +488,6 @@ class TalkerEngine:
         t = self.talker
         self.talker_tail = (TALKER_TAIL and self.wdt == torch.bfloat16 and
                             K.talker_tail_supported(t.H, t.I, t.Hq, t.D, t.qkv_w))
-        self.talker_step = (TALKER_STEP in (1, 2) and self.wdt == torch.bfloat16 and X16 and
-                            K.talker_step_supported(t.H, t.I, t.Hq, t.Hkv, t.D, t.n_layers))
         self._sessions: Dict[tuple, List[Session]] = {}
         torch.cuda.synchronize()
 
@@ -609,20 +605,7 @@ class TalkerEngine:
         # --- talker decode input and forward
         K.frame_embed(self.emb0, self.ecp, self.G, t.H, s.codes, codes_ld, s.step, s.trailing,
                       s.trailing.shape[1], s.pad_embed, s.x, B, x16=s.x16, step_stride=1)
-        if s.ts_tab is not None and s.meta.get("nsplit", 1) == 1:
-            m = s.meta
-            if TALKER_STEP == 1:  # every layer in one persistent launch
-                K.talker_step(s.ts_tab, t.n_layers, B, s.x, s.Lmax, t.cos, t.sin, m["rope_pos"], m["kv_pos"],
-                              m["row_start"], m["row_batch"], t.eps, s.ts_ws)
-            else:  # layer 0's q/k/v, then one launch per layer (attention .. the next layer's q/k/v)
-                K.gemm(s.x16, t.layers[0].qkv, s.ts_q[0], B, t.H, t.qkv_w, rms=True, eps=t.eps)
-                for li in range(t.n_layers):
-                    K.talker_step(s.ts_tab, 1, B, s.x, s.Lmax, t.cos, t.sin, m["rope_pos"], m["kv_pos"],
-                                  m["row_start"], m["row_batch"], t.eps, s.ts_ws, first_layer=li,
-                                  total_layers=t.n_layers, qkv_in=s.ts_q[li % 2],
-                                  qkv_out=s.ts_q[(li + 1) % 2] if li + 1 < t.n_layers else None)
-        else:
-            t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
+        t.forward(s.x, B, s.meta, s.kv, s.sc_t, s.Lmax, s.Lmax, decode=True, x16=s.x16)
         # next frame's past_hidden, also recorded as that frame's hidden state (hiddens[:, step + 1])
         K.rmsnorm(s.x, t.norm, t.eps, s.past_hidden, B, t.H, rec=s.hiddens, step=s.step, step_off=1, step_stride=1)
         K.gemm(s.past_hidden, self.codec_head, s.logits, B, t.H, self.V)
@@ -933,7 +916,11 @@ class TalkerEngine:
                     while harvests and harvests[0][-1].query():
                         i, hc, hh, hs, hf, _ = harvests.pop(0)
                         if hf is not None and int(hf[0]) != 0:  # never hand out a request decoded on stale partials
-                            check_handoffs([s])
+                            # the flag is session-wide: every request in flight is suspect -- stop and report them
+                            torch.cuda.synchronize(dev)
+                            _clear_flags(s)
+                            failed = {i} | {h[0] for h in harvests} | {r for r in slot_req if r >= 0}
+                            raise HandoffError(failed, queue)
                         # frames [0, F) are final: F = the first EOS in cb0 (within the row's frame range), else the
                         # row's frame count (max_new_tokens - 1)
                         F = min(int(hs[0]), cap_i[i])

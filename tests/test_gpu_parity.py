@@ -1131,6 +1131,31 @@ def test_stream_chunk_schedule_grows(tiny_models):
     kw["ignore_eos"] = True
     sizes = [pcm.numel() for b, pcm, last in model.stream(first_chunk_frames=1, chunk_frames=8, **kw) if b == 0]
     assert sizes[:5] == [1920 * 1 - 555, 1920 * 2, 1920 * 4, 1920 * 8, 1920 * 8], sizes
+    # a hand-off give-up during frame 0 (a session flag word set on the stream right behind the first frame) fails the
+    # request before the early one-frame first chunk's PCM is handed out (that chunk skips the EOS scan)
+    import qwen_tts.talker as T
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    orig = T.TalkerEngine._run_frame
+    ran = []
+
+    def run_frame(self, s, keys, use_graph=True, part="all"):
+        orig(self, s, keys, use_graph, part)
+        if not ran:
+            flag.fill_(1)
+        ran.append(part)
+    import pytest as _pt
+    mp = _pt.MonkeyPatch()
+    try:
+        mp.setattr(T, "_flag_words", lambda s: [flag])
+        mp.setattr(T.TalkerEngine, "_run_frame", run_frame)
+        got = []
+        with _pt.raises(RuntimeError, match="hand-off timed out"):
+            for item in model.stream(first_chunk_frames=1, chunk_frames=8, **kw):
+                got.append(item)
+        assert ran[0] == "cp" and not got, (ran, len(got))
+        assert int(flag.item()) == 0  # cleared for the session's next request
+    finally:
+        mp.undo()
 
 
 def test_prefill_graph_replay_matches_eager(tiny_models):

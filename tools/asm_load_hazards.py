@@ -73,6 +73,63 @@ def check(body):
     return bad
 
 
+def check_ring(body, n=16):
+    """The weight-ring loaders (talker_tail.hip) publish a slot behind an inline-asm `s_waitcnt vmcnt(n)` that is right
+    only if exactly the slot's n LDS-DMA transfers (global_load_lds_*, invisible to hipcc's counters) are the VMEM ops
+    issued since the previous slot: in layout order the run of VMEM instructions before each such wait must be n
+    global_load_lds and nothing else.  Returns [(line_no, problem)]; the number of waits checked is len of the second
+    list."""
+    bad, seen = [], []
+    in_asm = False
+    vmem = []  # VMEM instruction names in layout order since the last wait of any kind
+    for no, raw in enumerate(body.split("\n")):
+        line = raw.strip()
+        if line.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if line.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not line or line.startswith((";", ".")) or line.endswith(":"):
+            continue
+        op = line.split()[0]
+        if op == "s_waitcnt" and in_asm and re.search(rf"vmcnt\({n}\)", line):
+            seen.append(no)
+            run = 0
+            for v in reversed(vmem):
+                if "_lds_" not in v:
+                    break
+                run += 1
+            if run != n or any("_lds_" not in v for v in vmem[-n:]):
+                bad.append((no, f"vmcnt({n}) after a run of {run} global_load_lds (last VMEM ops {vmem[-(n + 2):]})"))
+            continue
+        if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+            vmem.append(op)
+    return bad, seen
+
+
+def check_r1(body):
+    """R1 publication order (MI355X_MICROARCH.md, visibility): every 32-bit sc1 flag store (global_store_dword ... sc1)
+    comes after an `s_waitcnt vmcnt(0)` that follows the last sc1 payload store (buffer_store_* ... sc1) before it in
+    layout order.  Returns ([(line_no, flag store)], flags checked)."""
+    bad, n = [], 0
+    undrained = False
+    for no, raw in enumerate(body.split("\n")):
+        line = raw.strip()
+        if not line or line.startswith((";", ".")) or line.endswith(":"):
+            continue
+        op = line.split()[0]
+        if op.startswith("buffer_store") and " sc1" in line:
+            undrained = True
+        elif op == "s_waitcnt" and "vmcnt(0)" in line:
+            undrained = False
+        elif op == "global_store_dword" and line.endswith("sc1"):
+            n += 1
+            if undrained:
+                bad.append((no, line))
+    return bad, n
+
+
 def main():
     asm = open(sys.argv[1]).read()
     keys = sys.argv[2:]

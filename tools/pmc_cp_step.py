@@ -37,8 +37,9 @@ for _ in range(4):
         Kn.cp_step(c.layers, lm[s], x, qkv, B, kc, vc, Lmax, s + 1, c.cos, c.sin, c.eps, logits, ws)
 torch.cuda.synchronize()
 assert int(ws[:4].view(torch.int32).item()) == 0, "hand-off flag set"
-L0 = c.layers[0]
-wb = sum(Wt.w.numel() * Wt.w.element_size() for Wt in (L0.qkv, L0.o, L0.gu, L0.down)) * len(c.layers)
+nb = lambda Wt: Wt.w.numel() * Wt.w.element_size()  # noqa: E731
+# layer 0's q/k/v weights are never read by a decode step (its rows come in through qkv0)
+wb = sum(nb(L.o) + nb(L.gu) + nb(L.down) + (nb(L.qkv) if i > 0 else 0) for i, L in enumerate(c.layers))
 kv = sum(len(c.layers) * B * c.Hkv * c.D * 2 * (2 * (s + 1) + 2) for s in steps) / len(steps)
 algo = int(wb + lm[1].w.numel() * 2 + kv + B * (c.H + c.qkv_w + V) * 4)
 print("algorithmic bytes per launch", algo)
