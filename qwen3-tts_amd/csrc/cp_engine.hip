@@ -70,9 +70,11 @@ struct Lay {
 constexpr size_t OFF_SG = Lay<16>::WS;                      // [8] u64 granules (256 B reserved)
 constexpr int E_SAMP = 30;                                  // its tag slot
 constexpr size_t WS_BYTES = OFF_SG + 256;
-// optional intermediates of layer 0 (a workspace this much larger records them; parity diagnostics): [4][MAXR][4096]
-// fp32 = x after the attention residual, the SwiGLU output, x after the MLP residual, the attention output
-constexpr size_t DBG_BYTES = (size_t)4 * MAXR * 4096 * 4;
+// optional per-stage intermediates of every layer (a workspace this much larger records them; the stage-by-stage parity
+// tests): fp32 [6 layers][DBG_KINDS][16 token rows][4096] -- kind 0 x after the attention residual, 1 the SwiGLU output,
+// 2 x after the MLP residual, 3 the attention output, 4 the layer's q/k/v rows (projected, before the q/k norm)
+constexpr int DBG_KINDS = 5, DBG_ROWS = 16;
+constexpr size_t DBG_BYTES = (size_t)6 * DBG_KINDS * DBG_ROWS * 4096 * 4;
 // ... and a workspace larger still records per-block phase timestamps (s_memrealtime, 100 MHz) after that:
 // [NB][64] u64 -- stamp 0 kernel start, 1 end, 2 + 12 l + k the layer-l events (tools/ce_debug.py names them)
 constexpr size_t STAMP_BYTES = (size_t)NB * 128 * 8;  // + [64, 128): sub-phase stamps of layer 2
@@ -138,7 +140,7 @@ struct Lds {
   __attribute__((aligned(16))) bf16_t zero[32];                // the A rows past the batch (MFMA rows >= R)
   const void* ptab[8][8];  // per-layer pointers [PT_*][layer]: one LDS read instead of a scalar kernarg miss per use
   float gath[MR / 8][NKV][32];                                 // the 8 head partials of the owned slices
-  __attribute__((aligned(16))) unsigned qs2[NW][NREP][D / 2];  // decode attention: q as bf16 pairs
+  __attribute__((aligned(16))) float qf[NW][NREP][D];          // decode attention: q (fp32)
   __attribute__((aligned(16))) unsigned kn2[NW][D / 2];        // the new key as bf16 pairs
   float vn[NW][D];                                             // the new value (bf16-rounded)
   // prefill attention (wave w = batch row w): q (fp32), k / v (bf16-rounded) at positions 0, 1
@@ -270,7 +272,9 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
   u64* gpart = (u64*)(ws + LY::OFF_PART);
   const rsrc_t wsr = mkr(ws, (unsigned)WS_BYTES);  // payload regions, addressed by byte offset
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);  // (low word: the error flag)
-  float* dbg = !PF && p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
+  float* dbg = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES) : nullptr;
+  // element (layer, kind, token row, column) of the stage record
+  auto dbgi = [](int l, int kind, int row, int col) { return (((size_t)l * DBG_KINDS + kind) * DBG_ROWS + row) * 4096 + col; };
   u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + DBG_BYTES + STAMP_BYTES)
                     ? (u64*)(ws + WS_BYTES + DBG_BYTES) + b * 128 : nullptr;
 #define CE_STAMP(k) \
@@ -507,6 +511,11 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) { xv[k] = __uint_as_float(a0[k]); xv[4 + k] = __uint_as_float(a1[k]); }
       }
+      if (dbg && cg == 0 && w < R) {  // (lane group vsel: q head 2h + vsel, k head h, v head h)
+        const int hh = vsel < NREP ? h * NREP + vsel : (vsel == NREP ? NQ + h : NQ + NKV + h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dbg[dbgi(l, 4, w, hh * D + e0 + i)] = xv[i];
+      }
       CE_STAMP(sb + 3);
       {  // q/k RMSNorm + RoPE (branch-free over the lane groups; the v group's result is discarded)
         const bool lo = e0 < half, normed = vsel <= NREP;
@@ -525,51 +534,51 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           xv[i] = normed ? ro : xv[i];
         }
       }
-      if (grp <= NREP) {
+      if (grp < NREP) {
+        *(f32x4_t*)&s.qf[w][grp][e0] = f32x4_t{xv[0], xv[1], xv[2], xv[3]};
+        *(f32x4_t*)&s.qf[w][grp][e0 + 4] = f32x4_t{xv[4], xv[5], xv[6], xv[7]};
+      } else if (grp == NREP) {
         u32x4_t pk2;
 #pragma unroll
         for (int i = 0; i < 4; ++i) pk2[i] = pack2bf_rne(xv[2 * i], xv[2 * i + 1]);
-        *(u32x4_t*)(grp < NREP ? &s.qs2[w][grp][e0 / 2] : &s.kn2[w][e0 / 2]) = pk2;
+        *(u32x4_t*)&s.kn2[w][e0 / 2] = pk2;
       } else if (grp == NREP + 1) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) s.vn[w][e0 + i] = bf2f(f2bf(xv[i]));
       }
       __syncthreads();
-      // attention of (row r, head h) over the cached keys [0, kvpos) + the new key (attn_oproj_hs_k, phase 3)
+      // attention of (row r, head h) over the cached keys [0, kvpos) + the new key, fp32 arithmetic on the bf16 keys /
+      // values as stored (q and the softmax weights stay fp32: only the output is rounded, as qt_decode_attention; the
+      // bf16 q / weight pairs of attn_oproj_hs_k's form cost ~1.4x its rounding error, tests/test_gpu_engine_stages.py)
       {
         const float scale = rsqrtf((float)D) * 1.4426950408889634f;
-        u32x4_t q2[NREP];
+        float qv[NREP][8];
 #pragma unroll
-        for (int j = 0; j < NREP; ++j) q2[j] = *(const u32x4_t*)&s.qs2[w][j][sub * 4];
+        for (int j = 0; j < NREP; ++j) {
+          const f32x4_t a = *(const f32x4_t*)&s.qf[w][j][sub * 8], b2 = *(const f32x4_t*)&s.qf[w][j][sub * 8 + 4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { qv[j][i] = a[i]; qv[j][4 + i] = b2[i]; }
+        }
         const u32x4_t k2n = *(const u32x4_t*)&s.kn2[w][sub * 4];
-        auto dot8 = [](const u32x4_t& a, const u32x4_t& bb) {
+        auto dotf = [](const float (&a)[8], const u32x4_t& bb) {  // fp32 q . bf16 pairs (dims 2i, 2i + 1)
           float d = 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const unsigned ai = a[i], bi = bb[i];
-            d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, ai), __builtin_bit_cast(bf16x2_t, bi), d,
-                                                false);
+            d = fmaf(a[2 * i], __uint_as_float(bb[i] << 16), d);
+            d = fmaf(a[2 * i + 1], __uint_as_float(bb[i] & 0xFFFF0000u), d);
           }
           return d;
         };
         float dd[NREP][IC], dn[NREP];
 #pragma unroll
         for (int j = 0; j < NREP; ++j) {
-          dn[j] = group_sum_dpp<LPK>(dot8(q2[j], k2n)) * scale;
+          dn[j] = group_sum_dpp<LPK>(dotf(qv[j], k2n)) * scale;
 #pragma unroll
           for (int c = 0; c < IC; ++c) {
-            const float d = group_sum_dpp<LPK>(dot8(q2[j], kq[c])) * scale;
+            const float d = group_sum_dpp<LPK>(dotf(qv[j], kq[c])) * scale;
             dd[j][c] = c * GPW + grp < nc ? d : -INFINITY;
           }
         }
-        unsigned vp[IC / 2][8];
-#pragma unroll
-        for (int pr = 0; pr < IC / 2; ++pr)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            vp[pr][i] = __builtin_amdgcn_perm(vq[2 * pr + 1][i], vq[2 * pr][i], 0x05040100u);
-            vp[pr][4 + i] = __builtin_amdgcn_perm(vq[2 * pr + 1][i], vq[2 * pr][i], 0x07060302u);
-          }
         float vnf[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) vnf[i] = s.vn[w][sub * 8 + i];
@@ -580,23 +589,21 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
           for (int c = 0; c < IC; ++c) mn = fmaxf(mn, dd[j][c]);
           const float en = grp == 0 ? exp2_hw(dn[j] - mn) : 0.f;
-          unsigned epk[IC / 2];
-#pragma unroll
-          for (int pr = 0; pr < IC / 2; ++pr)
-            epk[pr] = pack2bf_rne(exp2_hw(dd[j][2 * pr] - mn), exp2_hw(dd[j][2 * pr + 1] - mn));
+          float ev[IC];
           float ls = en;
 #pragma unroll
-          for (int pr = 0; pr < IC / 2; ++pr)
-            ls = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, epk[pr]),
-                                                 __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls, false);
+          for (int c = 0; c < IC; ++c) {
+            ev[c] = exp2_hw(dd[j][c] - mn);
+            ls += ev[c];
+          }
 #pragma unroll
           for (int d = 0; d < 8; ++d) {
             float acc = en * vnf[d];
-            const int vi = (d & 1) * 4 + (d >> 1);
 #pragma unroll
-            for (int pr = 0; pr < IC / 2; ++pr)
-              acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, epk[pr]),
-                                                    __builtin_bit_cast(bf16x2_t, vp[pr][vi]), acc, false);
+            for (int c = 0; c < IC; ++c) {
+              const unsigned u = vq[c][d >> 1];
+              acc = fmaf(ev[c], __uint_as_float((d & 1) ? (u & 0xFFFF0000u) : (u << 16)), acc);
+            }
             o[j][d] = acc;
           }
           m[j] = mn; lsum[j] = ls;
@@ -628,6 +635,13 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           const u32x4_t a0 = bld_c(wsr, o), a1 = bld_c(wsr, o + 16);
 #pragma unroll
           for (int k = 0; k < 4; ++k) { xv[t][k] = __uint_as_float(a0[k]); xv[t][4 + k] = __uint_as_float(a1[k]); }
+        }
+        if (dbg && cg == 0 && w < R) {  // (lane group grp: q head 2h + grp, k head h, v head h)
+          const int hh = grp < NREP ? h * NREP + grp : (grp == NREP ? NQ + h : NQ + NKV + h);
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dbg[dbgi(l, 4, 2 * w + t, hh * D + e0 + i)] = xv[t][i];
         }
         CE_STAMP(sb + 3);
         const bool lo = e0 < half, normed = grp <= NREP;
@@ -674,8 +688,10 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
       __syncthreads();
       CE_STAMP(sb + 4);
       if (AHEAD) load_p3(l, tid);
-      if (dbg && l == 0 && cg == 0 && w < R)
-        for (int j = lane; j < NREP * D; j += 64) dbg[((size_t)3 * MAXR + w) * 4096 + h * NREP * D + j] = bf2f(s.att[w][j]);
+      if (dbg && cg == 0 && w < R)
+        for (int t = 0; t < (PF ? 2 : 1); ++t)
+          for (int j = lane; j < NREP * D; j += 64)
+            dbg[dbgi(l, 3, PF ? 2 * w + t : w, h * NREP * D + j)] = bf2f(s.att[PF ? 2 * w + t : w][j]);
       // head h's K-slice of o_proj for columns 32cg .. 32cg + 32: wave w, fragments 2w, 2w + 1 of tile 2cg + w / 4
       {
         const int kt0 = (2 * w) % 8;
@@ -755,8 +771,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
             }
           }
           s.xown[lane >> 4][lane & 15] += v;
-          if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
-            dbg[((size_t)0 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
+          if (dbg && orow(lane >> 4) < RT)
+            dbg[dbgi(l, 0, orow(lane >> 4), 16 * to + (lane & 15))] = s.xown[lane >> 4][lane & 15];
         }
         publish_x16(0, tagof(5 * l + 2), lane);  // (the wave's own LDS writes above are complete: one wave, in order)
         if (EARLY) load_p3(l, tid);
@@ -809,9 +825,9 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           const unsigned o = (unsigned)LY::OFF_H + (unsigned)(rr * (I / 2) + tile * 4 + pp) * 4;
 #pragma unroll
           for (int rp = 0; rp < NREPL; ++rp) bst_c(hv, wsr, o + rp * (unsigned)LY::REPL_H);
-          if (dbg && l == 0) {
-            dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp] = __uint_as_float(hv << 16);
-            dbg[((size_t)1 * MAXR + rr) * 4096 + tile * 8 + 2 * pp + 1] = __uint_as_float(hv & 0xFFFF0000u);
+          if (dbg) {
+            dbg[dbgi(l, 1, rr, tile * 8 + 2 * pp)] = __uint_as_float(hv << 16);
+            dbg[dbgi(l, 1, rr, tile * 8 + 2 * pp + 1)] = __uint_as_float(hv & 0xFFFF0000u);
           }
         }
        }
@@ -884,8 +900,8 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
 #pragma unroll
           for (int ww = 0; ww < NW; ++ww) v += s.red[ww][lane & 15][lane >> 4];
           s.xown[lane >> 4][lane & 15] += v;
-          if (dbg && l == 0 && 2 * qo + (lane >> 4) < R)
-            dbg[((size_t)2 * MAXR + 2 * qo + (lane >> 4)) * 4096 + 16 * to + (lane & 15)] = s.xown[lane >> 4][lane & 15];
+          if (dbg && orow(lane >> 4) < RT)
+            dbg[dbgi(l, 2, orow(lane >> 4), 16 * to + (lane & 15))] = s.xown[lane >> 4][lane & 15];
         }
         publish_x16(1, tagof(5 * l + 4), lane);
         if (EARLY) next_w1();

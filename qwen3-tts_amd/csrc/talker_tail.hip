@@ -52,6 +52,10 @@ constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;
 constexpr size_t REPL_H = (size_t)MAXR * (I / 2) * 4;                  // [MAXR][I/2] bf16 pairs
 constexpr size_t WS_BYTES = OFF_H + NREPL * REPL_H;
 constexpr size_t STAMP_BYTES = (size_t)NB * 32 * 8;                    // optional per-block phase stamps
+// optional stage records after the stamps (a workspace STAMP_BYTES + DBG_BYTES larger; the stage-by-stage parity
+// tests): fp32 [4][MAXR][I] -- x after the o_proj residual, the SwiGLU output, x after the MLP residual, the next
+// layer's q/k/v rows
+constexpr size_t DBG_BYTES = (size_t)4 * MAXR * I * 4;
 
 struct TP {
   qt_talker_tail_args a;
@@ -92,6 +96,8 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   const unsigned ep = (unsigned)(ld_g((const u64*)(ws + OFF_ERR)) >> 32);
   auto tagof = [&](int e) { return ep * NEDGE + (unsigned)e + 1u; };
   u64* stamps = p.ws_bytes >= (long long)(WS_BYTES + STAMP_BYTES) ? (u64*)(ws + WS_BYTES) + b * 32 : nullptr;
+  float* dbg = p.ws_bytes >= (long long)(WS_BYTES + STAMP_BYTES + DBG_BYTES) ? (float*)(ws + WS_BYTES + STAMP_BYTES)
+                                                                              : nullptr;
 #define TT_STAMP(k) \
   if (kProbe && stamps && threadIdx.x == 0) stamps[(k)] = __builtin_amdgcn_s_memrealtime();
   TT_STAMP(0);
@@ -305,6 +311,9 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       if (owner) {
         pair_in(v, 0, tagof(E_PO));
         publish_x16(0, tagof(E_X1));
+        if (dbg)
+          for (int q = lane; q < MAXR * 16; q += 64)
+            if ((q >> 4) < R) dbg[((size_t)0 * MAXR + (q >> 4)) * I + 16 * ot + (q & 15)] = s.xo[q >> 4][q & 15];
       } else {
         pair_out(v, 0, tagof(E_PO));
       }
@@ -351,6 +360,11 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
           const unsigned o = (unsigned)OFF_H + (unsigned)(rr * (I / 2) + (b + NB * t3) * 4 + pp) * 4;
 #pragma unroll
           for (int rp = 0; rp < NREPL; ++rp) bst_c(s.hb[t3][rr][pp], wsr, o + rp * (unsigned)REPL_H);
+          if (dbg) {
+            const size_t e = ((size_t)1 * MAXR + rr) * I + (b + NB * t3) * 8 + 2 * pp;
+            dbg[e] = __uint_as_float(s.hb[t3][rr][pp] << 16);
+            dbg[e + 1] = __uint_as_float(s.hb[t3][rr][pp] & 0xFFFF0000u);
+          }
         }
       }
       drain_stores();
@@ -393,6 +407,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
         for (int q = lane; q < MAXR * 16; q += 64) {
           const int rr = q >> 4, c = q & 15;
           if (rr < R) p.x[(long long)rr * p.ldx + 16 * ot + c] = s.xo[rr][c];
+          if (dbg && rr < R) dbg[((size_t)2 * MAXR + rr) * I + 16 * ot + c] = s.xo[rr][c];
         }
         if (has_next) publish_x16(1, tagof(E_X2));
       } else {
@@ -424,6 +439,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       for (int i = 0; i < 4; ++i) {
         const int rr = lk * 4 + i;
         if (rr < R) p.qkv[(long long)rr * p.ldq + 16 * b + lm] = v[i] * s.rs[rr];
+        if (dbg && rr < R) dbg[((size_t)3 * MAXR + rr) * I + 16 * b + lm] = v[i] * s.rs[rr];
       }
     }
   }
@@ -452,6 +468,7 @@ bool tail_resident() {
 
 extern "C" long long qt_talker_tail_ws_bytes(void) { return (long long)WS_BYTES; }
 extern "C" long long qt_talker_tail_stamp_bytes(void) { return (long long)STAMP_BYTES; }
+extern "C" long long qt_talker_tail_dbg_bytes(void) { return (long long)(STAMP_BYTES + DBG_BYTES); }
 
 extern "C" int qt_talker_tail_supported(int H_, int I_, int Hq, int D_, int qkv_w) {
   return H_ == H && I_ == I && Hq * D_ == KO && qkv_w == NQKV && tail_resident();

@@ -116,7 +116,8 @@ EXPORTS = ["qt_gemm", "qt_tile_weight", "qt_qkv_post", "qt_attention", "qt_decod
            "qt_rmsnorm_rec", "qt_small_prefill_attention",
            "qt_decode_attn_oproj", "qt_attn_oproj_ws_bytes", "qt_attn_oproj_resident_blocks",
            "qt_cp_step", "qt_cp_prefill", "qt_cp_step_sampled", "qt_cp_step_ws_bytes", "qt_cp_step_supported", "qt_cp_step_dbg_bytes",
-           "qt_talker_tail", "qt_talker_tail_ws_bytes", "qt_talker_tail_stamp_bytes", "qt_talker_tail_supported",
+           "qt_talker_tail", "qt_talker_tail_ws_bytes", "qt_talker_tail_stamp_bytes", "qt_talker_tail_dbg_bytes",
+           "qt_talker_tail_supported",
            "qt_sample", "qt_rmsnorm", "qt_gather_rows", "qt_frame_embed", "qt_advance", "qt_advance_rows",
            "qt_rvq_gather", "qt_snake", "qt_dwconv_ln", "qt_clamp_pcm",
            "qt_pad_time", "qt_zero_tail", "qt_layernorm", "qt_rvq_encode", "qt_rvq_encode_ws_bytes", "qt_mel_logmag", "qt_time_stats",
@@ -178,7 +179,7 @@ def load_library(path: str = LIB_PATH):
         "qt_attn_oproj_resident_blocks": [],
         "qt_cp_step": [P, P], "qt_cp_prefill": [P, P], "qt_cp_step_sampled": [P, P, P], "qt_cp_step_ws_bytes": [], "qt_cp_step_dbg_bytes": [],
         "qt_cp_step_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
-        "qt_talker_tail": [P, P], "qt_talker_tail_ws_bytes": [], "qt_talker_tail_stamp_bytes": [],
+        "qt_talker_tail": [P, P], "qt_talker_tail_ws_bytes": [], "qt_talker_tail_stamp_bytes": [], "qt_talker_tail_dbg_bytes": [],
         "qt_talker_tail_supported": [c_int, c_int, c_int, c_int, c_int],
         "qt_pad_time": [P, c_ll, P, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_ll, P],
         "qt_zero_tail": [P, c_int, c_int, c_int, c_int, c_int, c_ll, P],

@@ -489,6 +489,7 @@ class TalkerEngine:
         self.talker_tail = (TALKER_TAIL and self.wdt == torch.bfloat16 and
                             K.talker_tail_supported(t.H, t.I, t.Hq, t.D, t.qkv_w))
         self._sessions: Dict[tuple, List[Session]] = {}
+        self._fence = None  # (event, stream) of the last frame issued (_fence_in / _fence_out)
         torch.cuda.synchronize()
 
     def _proj_table(self, emb, Hc):
@@ -1068,15 +1069,36 @@ class TalkerEngine:
         ns = attn_nsplit(keys)
         s.meta["nsplit"] = ns
         if not use_graph:
+            self._fence_in()
             with K.use_workspace(s.ws):
                 self._frame(s, part)
+            self._fence_out()
             return
         g = s.graphs.get((ns, part))
         if g is None:
             g = s.graphs[(ns, part)] = self._capture(s, part)
         if part == "all":
             s.graph = g
+        self._fence_in()
         g.replay()
+        self._fence_out()
+
+    # Frames of concurrent requests on different streams are serialised on the device: each persistent hand-off kernel
+    # of a frame (qt_cp_step / qt_cp_prefill, qt_talker_tail, the head-split attention + o_proj) needs all of its 256
+    # workgroups resident at once, one per CU, and two such launches running together could each hold part of the chip
+    # while waiting for blocks that cannot start (the bounded polls would then give up and fail both requests).  Each
+    # frame waits for the last frame issued on another stream (an event, no host sync); kernels without in-launch
+    # hand-offs (codec, prefill) still overlap freely.
+    def _fence_in(self):
+        cur = torch.cuda.current_stream(self.dev)
+        if self._fence is not None and self._fence[1] != cur:
+            cur.wait_event(self._fence[0])
+
+    def _fence_out(self):
+        cur = torch.cuda.current_stream(self.dev)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._fence = (ev, cur)
 
     def _capture(self, s: Session, part: str = "all"):
         # the graph must not see the prefill-time counter values: it only reads device memory

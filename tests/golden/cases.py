@@ -66,6 +66,11 @@ def full_cases():
         # (talker.attn_nsplit: 2 splits from 768 keys) and the refill-free frame graph of that split factor
         "cv17_b2_longctx": dict(preset="1.7b-customvoice", idx=65, texts=[800, 1000], languages=["english", "auto"],
                                 speakers=FULL_SPEAKERS[2:4], non_streaming_mode=True, max_new_tokens=49),
+        # the 4-split route: 2 rows x ~2,070 / 2,100-token texts, non-streaming, 16 frames -- talker caches of ~2,080-2,130
+        # keys, past talker.attn_nsplit's 2,048-key bound, so every frame runs the 4-split decode attention (the wrapper
+        # allows 2,048 new tokens and the model 4,096: W:329, M:2031)
+        "cv17_b2_longctx4": dict(preset="1.7b-customvoice", idx=66, texts=[2060, 2100], languages=["english", "auto"],
+                                 speakers=FULL_SPEAKERS[4:6], non_streaming_mode=True, max_new_tokens=17),
         # configs[1]: 0.6B CustomVoice, 1 utterance of 120 text tokens, non-streaming (Identity small_to_mtp, M:1174)
         "cv06_b1_nonstream": dict(preset="0.6b-customvoice", idx=61, texts=[120], languages=["english"],
                                   speakers=["vivian"], non_streaming_mode=True, max_new_tokens=49),

@@ -331,7 +331,7 @@ def make_full_bf16(only=None):
     full_<key>_refbf16.npz: the calibration of bf16 agreement (tests/test_gpu_full.py)."""
     import transformers.generation.logits_process as lp
     from cases import full_cases
-    for key in ("cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long", "cv17_b2_longctx"):
+    for key in ("cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long", "cv17_b2_longctx", "cv17_b2_longctx4"):
         if only and key != only:
             continue
         case = full_cases()[key]

@@ -14,6 +14,9 @@ the reference's own greedy codes (tests/golden/full_<case>.npz, written by make_
   cv17_b2_longctx    1.7B CustomVoice, 2 rows x 800 / 1000-token texts, non-streaming, 48 frames: talker caches of
                      ~810-1060 keys, so every frame runs the split-KV decode attention (2 splits from 768 keys,
                      talker.attn_nsplit) -- the long-cache route of M:634-657 / 787-801 up to W:329's lengths
+  cv17_b2_longctx4   1.7B CustomVoice, 2 rows x ~2,070 / 2,100-token texts, non-streaming, 16 frames: caches past
+                     2,048 keys, so every frame runs the 4-split decode attention (W:329 allows 2,048 new tokens,
+                     M:2031 4,096)
 
 Every greedy pick of the reference (talker cb0 and the code predictor's 15, [B, frames, 16]) carries its top-2
 margin of the processed scores (from the oracle, itself asserted bit-identical to the reference's codes when the
@@ -44,7 +47,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TOL_FP32 = 1e-4   # |fp32 GPU - fp32 CPU| logit differences measured here are < 1e-5
-REF_BF16 = ["cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long", "cv17_b2_longctx"]  # cases with a reference-bf16 fixture
+REF_BF16 = ["cv17_b8_stream", "cv06_b1_nonstream", "cv17_b2_long", "cv17_b2_longctx", "cv17_b2_longctx4"]  # cases with a reference-bf16 fixture
 
 
 def _ref_bf16_flip_margin():
@@ -133,7 +136,8 @@ def _check_free_run(codes, ref, margins, tol, label, require_full=False):
     return div
 
 
-KEYS = ["cv06_b1_nonstream", "cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone", "cv17_b2_long", "cv17_b2_longctx"]
+KEYS = ["cv06_b1_nonstream", "cv17_b8_stream", "vd17_b4_instruct", "base17_b2_clone", "cv17_b2_long", "cv17_b2_longctx",
+        "cv17_b2_longctx4"]
 
 
 @pytest.mark.parametrize("key", KEYS)
@@ -144,10 +148,11 @@ def test_full_dims_fp32_bit_exact(key):
     model = TTSModel(cfg, W, dtype="fp32")
     from cases import gen_kwargs
     codes, hid = model.generate(**kw, **gen_kwargs(case))
-    if key == "cv17_b2_longctx":  # the long-cache route ran: every frame graph of this request is a split-KV one
+    if key in ("cv17_b2_longctx", "cv17_b2_longctx4"):  # the long-cache route ran: every frame graph is a split one
         from qwen_tts.talker import attn_nsplit
+        want = 4 if key == "cv17_b2_longctx4" else 2
         used = {ns for s in model.engine.all_sessions() for ns, _ in s.graphs}
-        assert used and min(used) >= 2 and attn_nsplit(int(z["prompt_len"]) + 1) >= 2, used
+        assert used and min(used) >= want and attn_nsplit(int(z["prompt_len"]) + 1) >= want, used
     _check_free_run(codes, ref, z["margins"], TOL_FP32, f"{key} fp32")
     for j, h in enumerate(hid):
         assert _rel(h[:2].numpy(), z[f"hidden{j}_first"]) < 1e-4, (key, j)

@@ -6,6 +6,8 @@ import sys
 
 import torch
 
+DBG = 6 * 5 * 16 * 4096 * 4  # cp_engine.hip DBG_BYTES: [layer][kind][token row][4096] fp32 stage records
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "qwen3-tts_amd"), os.path.join(REPO, "tests")]
 from test_gpu_cp_engine import _chain, _cp_stack, _inputs, _rel  # noqa: E402
@@ -76,7 +78,7 @@ def layer0():
         Kn.cp_step(st.layers[:1], lm, x, qkv0, R, [k.clone() for k in kc], [v.clone() for v in vc], Lmax, pos, st.cos,
                    st.sin, st.eps, logits, ws)
         torch.cuda.synchronize()
-        d = ws[Kn.cp_step_ws_bytes():Kn.cp_step_ws_bytes() + 4 * 8 * 4096 * 4].view(torch.float32).view(4, 8, 4096)
+        d = ws[Kn.cp_step_ws_bytes():Kn.cp_step_ws_bytes() + DBG].view(torch.float32).view(6, 5, 16, 4096)[0]
         print(f"launch {it}: att rel {_rel(d[3, :R, :2048], att.float()):.3e}  x_attn rel {_rel(d[0, :R, :1024], xa):.3e}  "
               f"h rel {_rel(d[1, :R, :3072], h.float()):.3e}  x_mlp rel {_rel(d[2, :R, :1024], xm):.3e}", flush=True)
         for name, a, b in (("att", d[3, :R, :2048], att.float()), ("x_attn", d[0, :R, :1024], xa),
@@ -107,7 +109,7 @@ def stamps(R=8, reps=3):
     n = nws + int(_hip.lib().qt_cp_step_dbg_bytes())
     ws = torch.zeros(n, dtype=torch.uint8, device=dev)
     logits = torch.empty(R, lm.N, device=dev)
-    dbg_off = nws + 4 * 8 * 4096 * 4
+    dbg_off = nws + DBG
     tot = []
     for rep in range(reps):
         for pos in range(2, 16):
@@ -189,7 +191,7 @@ def pf_stamps(R=8, reps=3):
     nws = Kn.cp_step_ws_bytes()
     ws = torch.zeros(nws + int(_hip.lib().qt_cp_step_dbg_bytes()), dtype=torch.uint8, device=dev)
     logits = torch.empty(R, lm.N, device=dev)
-    dbg_off = nws + 4 * 8 * 4096 * 4
+    dbg_off = nws + DBG
     tot = []
     for rep in range(reps * 5):
         Kn.cp_prefill(st.layers, lm, x, R, kc, vc, Lmax, st.cos, st.sin, st.eps, logits, ws)
