@@ -13,10 +13,12 @@
 // wait for a hand-off -- and the consumers, whose own loads are only the hand-off polls and payloads, never wait
 // behind a weight round trip (vmcnt retires in order per wave).
 //
-// Geometry: 256 workgroups (one per CU, all resident -- the host checks the occupancy) x (8 consumer + 2 loader)
-// waves.  Block b:  o_proj and down: output tile t = b / 2 (16 of 2048 columns), K half b % 2 (split-K pair; the even
+// Geometry, for a talker of hidden size H and intermediate size I = 3 H (the config's; the 1.7B talker H 2048, the 0.6B
+// H 1024): NB = H / 8 workgroups (one per CU, all resident -- the host checks the occupancy) x (8 consumer + 2 loader)
+// waves.  Block b:  o_proj and down: output tile t = b / 2 (16 of H columns), K half b % 2 (split-K pair; the even
 // block OWNS x[rows][16t .. 16t + 16) and receives the odd block's partial as 8-byte {value, tag} granules);
-// gate/up: tiles b, b + 256, b + 512 (768 tiles of 8 gate + 8 up columns); next q/k/v: tile b (256 tiles).
+// gate/up: tiles b, b + NB, b + 2 NB (I / 8 tiles of 8 gate + 8 up columns); next q/k/v: tiles b, b + NB, ... (256
+// tiles of the 4096-wide q/k/v).
 // Hand-offs: x16 after each residual (all-to-all) and the SwiGLU rows (all-to-all) in the R1 form with one replica
 // per XCD (as qt_cp_step), the split-K pairs as granules.  Tags: epoch * 8 + edge + 1, the epoch a launch counter in
 // the workspace advanced by block 0 at the end.
@@ -28,59 +30,77 @@ namespace {
 
 using namespace qt_engine;
 
-constexpr int H = 2048, I = 6144, NQKV = 4096, KO = 2048;  // the 1.7B talker
-constexpr int NB = 256, NWC = 8, NWL = 2, NT = (NWC + NWL) * 64, MAXR = 8;
-constexpr int KTH = H / 32, KTI = I / 32, KTO = KO / 32;  // 64 / 192 / 64 k tiles
+constexpr int NQKV = 4096, KO = 2048;                    // q/k/v width, o_proj K (16 q heads x 128): both talkers
+constexpr int NBMAX = 256, NWC = 8, NWL = 2, NT = (NWC + NWL) * 64, MAXR = 8;
 constexpr int NSLOT = 5, SLOT = 16;                       // ring: 5 slots x 16 fragments (16 KiB)
-constexpr int XLD = H + 8, ALD = KO / 2 + 8, HLD = I / 2 + 8;
+constexpr int KTO = KO / 32, ALD = KO / 2 + 8;
 constexpr int NEDGE = 8;
 constexpr int NPRE = 8;  // ring slots a consumer wave holds in registers across a hand-off wait
 constexpr int E_PO = 0, E_X1 = 1, E_H = 2, E_PD = 3, E_X2 = 4;
-// slots per phase: o_proj 32 k tiles, gate/up 3 tiles x 64, down 96 k tiles, q/k/v 64
-constexpr int S_O = KTO / 2 / SLOT, S_GU = 3 * KTH / SLOT, S_D = KTI / 2 / SLOT, S_Q = KTH / SLOT;
-static_assert(S_O == 2 && S_GU == 12 && S_D == 6 && S_Q == 4, "slot plan");
+constexpr int HMAX = 2048, IMAX = 6144;
 
-// workspace (bytes)
+// per-config constants: H hidden, I intermediate
+template <int H_, int I_>
+struct TC {
+  static constexpr int H = H_, I = I_;
+  static constexpr int NB = H / 8;                        // workgroups: split-K pairs over the H / 16 output tiles
+  static constexpr int NGU = I / H;                       // gate/up tiles per block (I / 8 tiles over NB blocks)
+  static constexpr int NQT = (NQKV / 16) / NB;            // next-layer q/k/v tiles per block
+  static constexpr int KTH = H / 32, KTI = I / 32;        // k tiles
+  static constexpr int SPT = KTH / SLOT;                  // ring slots per H-deep tile (gate/up, q/k/v)
+  static constexpr int XLD = H + 8, HLD = I / 2 + 8;
+  // slots per phase: o_proj 32 k tiles, gate/up NGU tiles x KTH, down KTI / 2 k tiles, q/k/v NQT tiles x KTH
+  static constexpr int S_O = KTO / 2 / SLOT, S_GU = NGU * SPT, S_D = KTI / 2 / SLOT, S_Q = NQT * SPT;
+  static_assert(I % H == 0 && (NQKV / 16) % NB == 0 && KTH % SLOT == 0 && (KTI / 2) % SLOT == 0, "geometry");
+  static_assert(S_O == 2 && S_D <= NPRE && NB <= NBMAX, "slot plan");
+  static constexpr int NXK = H / 512, NHK = I / 1024;     // 16-byte loads per lane: an x16 row, a SwiGLU K half
+};
+
+// workspace (bytes; one layout, sized for the largest config)
 constexpr size_t OFF_ERR = 0, OFF_EPOCH = 4;
 constexpr int NREPL = 8;
 constexpr int FL_X1 = 0, FL_H = 1, FL_X2 = 2;
-constexpr size_t OFF_FLAGS = 256, REPL_FLAGS = (size_t)3 * NB * 4;
+constexpr size_t OFF_FLAGS = 256, REPL_FLAGS = (size_t)3 * NBMAX * 4;
 constexpr size_t OFF_PART = OFF_FLAGS + NREPL * REPL_FLAGS;             // [2][128 tiles][MAXR][16] granules
 constexpr size_t OFF_X16 = OFF_PART + (size_t)2 * 128 * MAXR * 16 * 8;
-constexpr size_t REPL_X16 = (size_t)2 * MAXR * (H / 2) * 4;            // [2 bufs][MAXR][H/2] bf16 pairs
+constexpr size_t REPL_X16 = (size_t)2 * MAXR * (HMAX / 2) * 4;         // [2 bufs][MAXR][H/2] bf16 pairs
 constexpr size_t OFF_H = OFF_X16 + NREPL * REPL_X16;
-constexpr size_t REPL_H = (size_t)MAXR * (I / 2) * 4;                  // [MAXR][I/2] bf16 pairs
+constexpr size_t REPL_H = (size_t)MAXR * (IMAX / 2) * 4;               // [MAXR][I/2] bf16 pairs
 constexpr size_t WS_BYTES = OFF_H + NREPL * REPL_H;
-constexpr size_t STAMP_BYTES = (size_t)NB * 32 * 8;                    // optional per-block phase stamps
+constexpr size_t STAMP_BYTES = (size_t)NBMAX * 32 * 8;                 // optional per-block phase stamps
 // optional stage records after the stamps (a workspace STAMP_BYTES + DBG_BYTES larger; the stage-by-stage parity
-// tests): fp32 [4][MAXR][I] -- x after the o_proj residual, the SwiGLU output, x after the MLP residual, the next
+// tests): fp32 [4][MAXR][IMAX] -- x after the o_proj residual, the SwiGLU output, x after the MLP residual, the next
 // layer's q/k/v rows
-constexpr size_t DBG_BYTES = (size_t)4 * MAXR * I * 4;
+constexpr size_t DBG_BYTES = (size_t)4 * MAXR * IMAX * 4;
 
 struct TP {
   qt_talker_tail_args a;
   int spin;
 };
 
+template <class C>
 struct TLds {
   __attribute__((aligned(16))) unsigned char ring[NSLOT][SLOT * 1024];
   union {
-    bf16_t xa[MAXR][XLD];  // x16 rows: the A operand of gate/up and q/k/v
-    bf16_t aa[MAXR][ALD];  // the attention rows' K half: the A operand of o_proj
-    bf16_t ha[MAXR][HLD];  // the SwiGLU rows' K half: the A operand of down
+    bf16_t xa[MAXR][C::XLD];  // x16 rows: the A operand of gate/up and q/k/v
+    bf16_t aa[MAXR][ALD];     // the attention rows' K half: the A operand of o_proj
+    bf16_t ha[MAXR][C::HLD];  // the SwiGLU rows' K half: the A operand of down
   } a;
   float red[2][NWC][64][4];                     // per-wave MFMA partials (double-buffered: gate/up tiles)
   float rs[MAXR];                               // 1 / rms per row
   float xo[MAXR][16];                           // owner: the residual slice (fp32)
-  unsigned hb[3][MAXR][4];                      // this block's SwiGLU output pairs
+  unsigned hb[C::NGU][MAXR][4];                 // this block's SwiGLU output pairs
   __attribute__((aligned(16))) bf16_t zero[32];
   unsigned full[NSLOT];                         // ring slot s % NSLOT holds sequence number s (+1)
   unsigned done[NWC];                           // consumer wave w has finished with sequences < done[w]
 };
 
+template <class C>
 __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
+  constexpr int H = C::H, I = C::I, NB = C::NB, KTH = C::KTH, KTI = C::KTI, SPT = C::SPT, NGU = C::NGU;
+  constexpr int S_O = C::S_O, S_GU = C::S_GU, S_D = C::S_D, S_Q = C::S_Q, XLD = C::XLD, HLD = C::HLD;
   const qt_talker_tail_args& p = pk.a;
-  __shared__ TLds s;
+  __shared__ TLds<C> s;
   __shared__ unsigned cb_cnt, cb_gen;
   const int b = blockIdx.x;
   const int ot = b >> 1, kh = b & 1;  // o_proj / down: tile, K half
@@ -117,9 +137,9 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       const void* W;
       int tile, kt0, KT;
       if (sq < S_O) { W = p.w_o; tile = ot; kt0 = kh * (KTO / 2) + SLOT * sq; KT = KTO; }
-      else if (sq < S_O + S_GU) { const int j = sq - S_O; W = p.w_gu; tile = b + NB * (j / 4); kt0 = SLOT * (j % 4); KT = KTH; }
+      else if (sq < S_O + S_GU) { const int j = sq - S_O; W = p.w_gu; tile = b + NB * (j / SPT); kt0 = SLOT * (j % SPT); KT = KTH; }
       else if (sq < S_O + S_GU + S_D) { const int j = sq - S_O - S_GU; W = p.w_down; tile = ot; kt0 = kh * (KTI / 2) + SLOT * j; KT = KTI; }
-      else { const int j = sq - S_O - S_GU - S_D; W = p.w_qkv_next; tile = b; kt0 = SLOT * j; KT = KTH; }
+      else { const int j = sq - S_O - S_GU - S_D; W = p.w_qkv_next; tile = b + NB * (j / SPT); kt0 = SLOT * (j % SPT); KT = KTH; }
       const int slot = sq % NSLOT;
       if (sq >= NSLOT) {  // the slot's previous sequence consumed by every consumer wave
         for (int spins = 0;; ++spins) {
@@ -172,13 +192,13 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   // registers and releases the slots: the ring (5 LDS slots, ~3 us of stream) would otherwise fill during the wait
   // and stall the loaders; registers extend it by NPRE slots.
   u32x4_t pf[2 * NPRE];
-  auto pretake = [&](int n) {
+  auto pretake = [&](int n) {  // (n <= NPRE)
 #pragma unroll
     for (int k = 0; k < NPRE; ++k)
       if (k < n) take(pf[2 * k], pf[2 * k + 1]);
   };
-  auto frags = [&](int k, u32x4_t& f0, u32x4_t& f1) {  // slot k of the phase: pre-taken or from the ring
-    if (k < NPRE) { f0 = pf[2 * k]; f1 = pf[2 * k + 1]; } else take(f0, f1);
+  auto frags = [&](int k, int npre, u32x4_t& f0, u32x4_t& f1) {  // slot k of the phase: pre-taken or from the ring
+    if (k < npre) { f0 = pf[2 * k]; f1 = pf[2 * k + 1]; } else take(f0, f1);
   };
   auto wait_flags = [&](unsigned off, int n, unsigned tag) {
     if (w == 0) {
@@ -212,13 +232,13 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   auto stage_x16 = [&](int buf) {
     const int row = tid >> 6;
     const unsigned base = (unsigned)(OFF_X16 + myrep * REPL_X16 + (size_t)buf * MAXR * (H / 2) * 4);
-    u32x4_t v[4];
+    u32x4_t v[C::NXK];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < C::NXK; ++k)
       v[k] = row < R ? bld_c(wsr, base + (unsigned)(row * (H / 2)) * 4 + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < C::NXK; ++k) {
       *(u32x4_t*)&s.a.xa[row][(lane + 64 * k) * 8] = v[k];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -313,7 +333,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
         publish_x16(0, tagof(E_X1));
         if (dbg)
           for (int q = lane; q < MAXR * 16; q += 64)
-            if ((q >> 4) < R) dbg[((size_t)0 * MAXR + (q >> 4)) * I + 16 * ot + (q & 15)] = s.xo[q >> 4][q & 15];
+            if ((q >> 4) < R) dbg[((size_t)0 * MAXR + (q >> 4)) * IMAX + 16 * ot + (q & 15)] = s.xo[q >> 4][q & 15];
       } else {
         pair_out(v, 0, tagof(E_PO));
       }
@@ -322,18 +342,19 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   }
   // ------------------------------------------------------------------ gate/up (3 tiles) + SwiGLU
   {
-    pretake(NPRE);
-    wait_flags(fl_off(myrep, FL_X1), 128, tagof(E_X1));
+    constexpr int npre = S_GU < NPRE ? S_GU : NPRE;
+    pretake(npre);
+    wait_flags(fl_off(myrep, FL_X1), H / 16, tagof(E_X1));
     TT_STAMP(3);
     stage_x16(0);
     TT_STAMP(4);
 #pragma unroll
-    for (int t3 = 0; t3 < 3; ++t3) {
+    for (int t3 = 0; t3 < NGU; ++t3) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < SPT; ++j) {
         u32x4_t f0, f1;
-        frags(4 * t3 + j, f0, f1);
+        frags(SPT * t3 + j, npre, f0, f1);
         const int kt = SLOT * j + 2 * w;
         acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt), f0, acc);
         acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
@@ -354,14 +375,14 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
       }
     }
     if (w == 0) {  // this block's 3 tiles x 8 rows x 4 pairs to every replica, drain, flags
-      for (int q = lane; q < 3 * MAXR * 4; q += 64) {
+      for (int q = lane; q < NGU * MAXR * 4; q += 64) {
         const int t3 = q / (MAXR * 4), rr = (q >> 2) % MAXR, pp = q & 3;
         if (rr < R) {
           const unsigned o = (unsigned)OFF_H + (unsigned)(rr * (I / 2) + (b + NB * t3) * 4 + pp) * 4;
 #pragma unroll
           for (int rp = 0; rp < NREPL; ++rp) bst_c(s.hb[t3][rr][pp], wsr, o + rp * (unsigned)REPL_H);
           if (dbg) {
-            const size_t e = ((size_t)1 * MAXR + rr) * I + (b + NB * t3) * 8 + 2 * pp;
+            const size_t e = ((size_t)1 * MAXR + rr) * IMAX + (b + NB * t3) * 8 + 2 * pp;
             dbg[e] = __uint_as_float(s.hb[t3][rr][pp] << 16);
             dbg[e + 1] = __uint_as_float(s.hb[t3][rr][pp] & 0xFFFF0000u);
           }
@@ -380,11 +401,11 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
     {  // the SwiGLU rows' K half: thread -> row tid / 64, 6 x 16 B
       const int row = tid >> 6;
       const unsigned base = (unsigned)(OFF_H + myrep * REPL_H) + (unsigned)(row * (I / 2) + kh * (I / 4)) * 4;
-      u32x4_t v[6];
+      u32x4_t v[C::NHK];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) v[k] = row < R ? bld_c(wsr, base + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
+      for (int k = 0; k < C::NHK; ++k) v[k] = row < R ? bld_c(wsr, base + (lane + 64 * k) * 16) : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int k = 0; k < 6; ++k) *(u32x4_t*)&s.a.ha[row][(lane + 64 * k) * 8] = v[k];
+      for (int k = 0; k < C::NHK; ++k) *(u32x4_t*)&s.a.ha[row][(lane + 64 * k) * 8] = v[k];
     }
     cons_sync<NWC>(cb, cg, pk.spin, err);
     TT_STAMP(7);
@@ -392,7 +413,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
 #pragma unroll
     for (int j = 0; j < S_D; ++j) {
       u32x4_t f0, f1;
-      frags(j, f0, f1);
+      frags(j, S_D, f0, f1);
       const int kt = SLOT * j + 2 * w;
       acc = mfma(afrag(&s.a.ha[0][0], HLD, R, kt), f0, acc);
       acc = mfma(afrag(&s.a.ha[0][0], HLD, R, kt + 1), f1, acc);
@@ -407,7 +428,7 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
         for (int q = lane; q < MAXR * 16; q += 64) {
           const int rr = q >> 4, c = q & 15;
           if (rr < R) p.x[(long long)rr * p.ldx + 16 * ot + c] = s.xo[rr][c];
-          if (dbg && rr < R) dbg[((size_t)2 * MAXR + rr) * I + 16 * ot + c] = s.xo[rr][c];
+          if (dbg && rr < R) dbg[((size_t)2 * MAXR + rr) * IMAX + 16 * ot + c] = s.xo[rr][c];
         }
         if (has_next) publish_x16(1, tagof(E_X2));
       } else {
@@ -418,28 +439,33 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   }
   // ------------------------------------------------------------------ next layer's q/k/v (input RMSNorm folded)
   if (has_next) {
-    pretake(S_Q);
-    wait_flags(fl_off(myrep, FL_X2), 128, tagof(E_X2));
+    constexpr int npre = S_Q < NPRE ? S_Q : NPRE;
+    pretake(npre);
+    wait_flags(fl_off(myrep, FL_X2), H / 16, tagof(E_X2));
     stage_x16(1);
     TT_STAMP(9);
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < S_Q; ++j) {
-      u32x4_t f0, f1;
-      frags(j, f0, f1);
-      const int kt = SLOT * j + 2 * w;
-      acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt), f0, acc);
-      acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
-    }
-    red_put(0, acc);
-    cons_sync<NWC>(cb, cg, pk.spin, err);
-    if (w == 0) {
-      const f32x4_t v = red_sum(0);
+    for (int tq = 0; tq < C::NQT; ++tq) {  // q/k/v tiles b + NB tq
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = lk * 4 + i;
-        if (rr < R) p.qkv[(long long)rr * p.ldq + 16 * b + lm] = v[i] * s.rs[rr];
-        if (dbg && rr < R) dbg[((size_t)3 * MAXR + rr) * I + 16 * b + lm] = v[i] * s.rs[rr];
+      for (int j = 0; j < SPT; ++j) {
+        u32x4_t f0, f1;
+        frags(SPT * tq + j, npre, f0, f1);
+        const int kt = SLOT * j + 2 * w;
+        acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt), f0, acc);
+        acc = mfma(afrag(&s.a.xa[0][0], XLD, R, kt + 1), f1, acc);
+      }
+      red_put(tq & 1, acc);
+      cons_sync<NWC>(cb, cg, pk.spin, err);
+      if (w == 0) {
+        const f32x4_t v = red_sum(tq & 1);
+        const int col = 16 * (b + NB * tq) + lm;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = lk * 4 + i;
+          if (rr < R) p.qkv[(long long)rr * p.ldq + col] = v[i] * s.rs[rr];
+          if (dbg && rr < R) dbg[((size_t)3 * MAXR + rr) * IMAX + col] = v[i] * s.rs[rr];
+        }
       }
     }
   }
@@ -450,19 +476,23 @@ __global__ __launch_bounds__(NT) void talker_tail_k(TP pk) {
   TT_STAMP(10);
 }
 
+template <class C>
 bool tail_resident() {
   static int cap[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
   if (cap[dev] == 0) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)talker_tail_k, NT, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)talker_tail_k<C>, NT, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return false;
     cap[dev] = std::max(1, per_cu * cus);
   }
-  return cap[dev] >= NB;
+  return cap[dev] >= C::NB;
 }
+
+using C17 = TC<2048, 6144>;  // the 1.7B talker
+using C06 = TC<1024, 3072>;  // the 0.6B talker
 
 }  // namespace
 
@@ -471,7 +501,10 @@ extern "C" long long qt_talker_tail_stamp_bytes(void) { return (long long)STAMP_
 extern "C" long long qt_talker_tail_dbg_bytes(void) { return (long long)(STAMP_BYTES + DBG_BYTES); }
 
 extern "C" int qt_talker_tail_supported(int H_, int I_, int Hq, int D_, int qkv_w) {
-  return H_ == H && I_ == I && Hq * D_ == KO && qkv_w == NQKV && tail_resident();
+  if (Hq * D_ != KO || qkv_w != NQKV) return 0;
+  if (H_ == C17::H && I_ == C17::I) return tail_resident<C17>();
+  if (H_ == C06::H && I_ == C06::I) return tail_resident<C06>();
+  return 0;
 }
 
 extern "C" int qt_talker_tail(const qt_talker_tail_args* a, void* stream) {
@@ -479,10 +512,13 @@ extern "C" int qt_talker_tail(const qt_talker_tail_args* a, void* stream) {
   if (!a->ws || a->ws_bytes < (long long)WS_BYTES || !a->att || !a->x || !a->w_o || !a->w_gu || !a->w_down)
     return QT_ERR_ARG;
   if (a->w_qkv_next && !a->qkv) return QT_ERR_ARG;
-  if (a->lda < KO || a->ldx < H || (a->w_qkv_next && a->ldq < NQKV)) return QT_ERR_SHAPE;
+  const bool big = a->H == C17::H && a->I == C17::I, small = a->H == C06::H && a->I == C06::I;
+  if (!big && !small) return QT_ERR_SHAPE;
+  if (a->lda < KO || a->ldx < a->H || (a->w_qkv_next && a->ldq < NQKV)) return QT_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(a->att) | (a->lda * 2)) & 15) return QT_ERR_ARG;  // 16-byte row loads
-  if (!tail_resident()) return QT_ERR_SHAPE;
+  if (big ? !tail_resident<C17>() : !tail_resident<C06>()) return QT_ERR_SHAPE;
   static const int spin = std::max(1000, qt_knob("QT_TT_SPIN", 200000));
-  hipLaunchKernelGGL(talker_tail_k, dim3(NB), dim3(NT), 0, (hipStream_t)stream, TP{*a, spin});
+  if (big) hipLaunchKernelGGL(talker_tail_k<C17>, dim3(C17::NB), dim3(NT), 0, (hipStream_t)stream, TP{*a, spin});
+  else hipLaunchKernelGGL(talker_tail_k<C06>, dim3(C06::NB), dim3(NT), 0, (hipStream_t)stream, TP{*a, spin});
   return hipGetLastError() == hipSuccess ? QT_OK : QT_ERR_LAUNCH;
 }

@@ -94,7 +94,7 @@ class TalkerStepArgs(ctypes.Structure):
 class TalkerTailArgs(ctypes.Structure):
     _fields_ = [("R", c_int), ("eps", ctypes.c_float), ("att", c_void_p), ("lda", c_ll), ("x", c_void_p), ("ldx", c_ll),
                 ("w_o", c_void_p), ("w_gu", c_void_p), ("w_down", c_void_p), ("w_qkv_next", c_void_p),
-                ("qkv", c_void_p), ("ldq", c_ll), ("ws", c_void_p), ("ws_bytes", c_ll)]
+                ("qkv", c_void_p), ("ldq", c_ll), ("ws", c_void_p), ("ws_bytes", c_ll), ("H", c_int), ("I", c_int)]
 
 
 class SampleArgs(ctypes.Structure):

@@ -350,6 +350,7 @@ def talker_tail(att, x, R, layer, next_layer, qkv, eps, ws):
     a.w_qkv_next = ptr(next_layer.qkv.w) if next_layer is not None else None
     a.qkv, a.ldq = (ptr(qkv), qkv.stride(0)) if next_layer is not None else (None, 0)
     a.ws, a.ws_bytes = ptr(ws), ws.numel() * ws.element_size()
+    a.H, a.I = layer.o.N, layer.gu.N // 2  # the config's hidden / intermediate sizes (the engine is built for both talkers)
     check(_hip.lib().qt_talker_tail(ctypes.byref(a), stream()), "qt_talker_tail")
 
 

@@ -309,11 +309,11 @@ def test_cp_prefill_stages_vs_fp64(R):
 
 
 # ---------------------------------------------------------------------------------------------- talker tail
-TH, TI, THQ, TD, TQKV = 2048, 6144, 16, 128, 4096
+THQ, TD, TQKV, TIMAX = 16, 128, 4096, 6144  # (the stage records' row stride is the largest intermediate size)
 
 
 class _TL:
-    def __init__(self, g, dev):
+    def __init__(self, g, dev, TH, TI):
         from qwen_tts import kernels as Kn
         r = lambda *s: (torch.randn(*s, generator=g) * 0.02)  # noqa: E731
         gam = lambda n: (1 + 0.1 * torch.randn(n, generator=g))  # noqa: E731
@@ -328,14 +328,16 @@ class _TL:
         self.r_gate, self.r_up, self.r_down = eff(wg, gpost), eff(wu, gpost), wd.to(dev).to(torch.bfloat16)
 
 
+@pytest.mark.parametrize("dims", [(2048, 6144), (1024, 3072)])  # the 1.7B / 0.6B talkers
 @pytest.mark.parametrize("R", [8, 1])
-def test_talker_tail_stages_vs_fp64(R):
+def test_talker_tail_stages_vs_fp64(R, dims):
     from qwen_tts import _hip, kernels as Kn
     dev = _dev()
+    TH, TI = dims
     if not Kn.talker_tail_supported(TH, TI, THQ, TD, TQKV):
         pytest.skip("qt_talker_tail not supported on this device")
     g = torch.Generator().manual_seed(41)
-    L, Ln = _TL(g, dev), _TL(g, dev)
+    L, Ln = _TL(g, dev, TH, TI), _TL(g, dev, TH, TI)
     eps = 1e-6
     att = torch.randn(R, THQ * TD, generator=g).to(dev).to(torch.bfloat16)
     x = torch.randn(R, TH, generator=g).to(dev)
@@ -355,8 +357,8 @@ def test_talker_tail_stages_vs_fp64(R):
     Kn.talker_tail(att, xe, R, L, Ln, qe, eps, ws)
     torch.cuda.synchronize()
     assert int(ws[:4].view(torch.int32).item()) == 0
-    d = ws[nws + int(_hip.lib().qt_talker_tail_stamp_bytes()):].view(torch.float32)[:4 * 8 * TI].view(4, 8, TI)
-    eng = dict(x_attn=d[0, :R, :TH], h=d[1, :R], x_mlp=d[2, :R, :TH], qkv=d[3, :R, :TQKV])
+    d = ws[nws + int(_hip.lib().qt_talker_tail_stamp_bytes()):].view(torch.float32)[:4 * 8 * TIMAX].view(4, 8, TIMAX)
+    eng = dict(x_attn=d[0, :R, :TH], h=d[1, :R, :TI], x_mlp=d[2, :R, :TH], qkv=d[3, :R, :TQKV])
     assert torch.equal(eng["x_mlp"], xe) and torch.equal(eng["qkv"], qe)  # the records are the outputs
 
     def errs(p):
@@ -366,7 +368,7 @@ def test_talker_tail_stages_vs_fp64(R):
         e["qkv"] = _rel(p["qkv"], _rms_lin(p["x_mlp"], Ln.r_qkv, eps))
         return e
     ee, ce = errs(eng), errs(chain)
-    print(f"\n  talker_tail R={R} (engine / chain error vs fp64): " +
+    print(f"\n  talker_tail H={TH} R={R} (engine / chain error vs fp64): " +
           "  ".join(f"{k} {ee[k]:.2e}/{ce[k]:.2e}" for k in ee))
     for k in ee:
         assert ee[k] < 1e-2, (k, ee[k])

@@ -2,7 +2,7 @@
 gate/up, down, next q/k/v GEMVs), 1.7B talker shapes, 28 layers of distinct random weights (every launch streams its
 weights from HBM, as in a frame), B rows; HIP graphs replayed between HIP events.  With the probe library and
 TT_STAMPS=1: per-phase timestamps of one launch (median / max over blocks).
-    python tools/tt_bench.py [B]"""
+    python tools/tt_bench.py [B] [H]   (H 2048: the 1.7B talker, I 6144; H 1024: the 0.6B talker, I 3072)"""
 import os
 import sys
 
@@ -11,7 +11,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "qwen3-tts_amd"), os.path.join(REPO, "tests")]
 from qwen_tts import _hip, kernels as Kn  # noqa: E402
-from test_gpu_talker_tail import _L, H, I, HQ, D, QKV  # noqa: E402
+from test_gpu_talker_tail import _L, HQ, D, QKV  # noqa: E402
 
 
 def graph_us(run, reps, dev):
@@ -35,9 +35,11 @@ def graph_us(run, reps, dev):
 def main():
     dev = torch.device("cuda:0")
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    H = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    I = 3 * H
     nl = 28
     g = torch.Generator().manual_seed(1)
-    layers = [_L(g, dev) for _ in range(nl + 1)]
+    layers = [_L(g, dev, H, I) for _ in range(nl + 1)]
     att = torch.randn(B, HQ * D, device=dev).to(torch.bfloat16)
     x = torch.randn(B, H, device=dev)
     x16 = x.to(torch.bfloat16)
@@ -63,13 +65,14 @@ def main():
     for name, fn in (("chain (4 GEMV launches)", chain), ("qt_talker_tail", tail), ("chain (4 GEMV launches)", chain),
                      ("qt_talker_tail", tail)):
         us = graph_us(fn, 5, dev) / nl
-        print(f"B={B} {name}: {us:.2f} us per layer = {wb / (us * 1e-6) / 1e12:.2f} TB/s of weights", flush=True)
+        print(f"H={H} B={B} {name}: {us:.2f} us per layer = {wb / (us * 1e-6) / 1e12:.2f} TB/s of weights", flush=True)
     print("error flag", int(ws[:4].view(torch.int32).item()))
     if os.environ.get("TT_STAMPS") and _hip.PROBE:
         import numpy as np
         Kn.talker_tail(att, x, B, layers[3], layers[4], qkv, eps, ws)
         torch.cuda.synchronize()
-        t = ws[Kn.talker_tail_ws_bytes():].view(torch.int64).view(256, 32).cpu().numpy().astype(np.float64) * 0.01
+        t = ws[Kn.talker_tail_ws_bytes():].view(torch.int64)[:H // 8 * 32].view(H // 8, 32).cpu().numpy()
+        t = t.astype(np.float64) * 0.01
         t0 = t[:, 0].min()
         names = ["start", "staged", "o done", "x1 in", "x16 staged", "h pub", "h in", "h staged", "down done",
                  "qkv staged", "end"]
