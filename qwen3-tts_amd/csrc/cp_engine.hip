@@ -560,28 +560,47 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
           for (int i = 0; i < 4; ++i) { qv[j][i] = a[i]; qv[j][4 + i] = b2[i]; }
         }
         const u32x4_t k2n = *(const u32x4_t*)&s.kn2[w][sub * 4];
-        auto dotf = [](const float (&a)[8], const u32x4_t& bb) {  // fp32 q . bf16 pairs (dims 2i, 2i + 1)
-          float d = 0.f;
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        // bf16 pair (dims 2i, 2i + 1) -> fp32 pair; each key / value fragment unpacked once for both q heads, the dot
+        // products and the weighted value sums as packed fp32 FMAs (v_pk_fma_f32: two per instruction)
+        auto unp = [](unsigned u) { return f2v{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)}; };
+        f2v qp[NREP][4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            d = fmaf(a[2 * i], __uint_as_float(bb[i] << 16), d);
-            d = fmaf(a[2 * i + 1], __uint_as_float(bb[i] & 0xFFFF0000u), d);
-          }
-          return d;
+        for (int j = 0; j < NREP; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) qp[j][i] = f2v{qv[j][2 * i], qv[j][2 * i + 1]};
+        auto dot_pk = [&](int j, const f2v (&kf)[4]) {
+          f2v acc = qp[j][0] * kf[0];
+#pragma unroll
+          for (int i = 1; i < 4; ++i) acc = qp[j][i] * kf[i] + acc;
+          return acc.x + acc.y;
         };
         float dd[NREP][IC], dn[NREP];
+        {
+          f2v kf[4];
 #pragma unroll
-        for (int j = 0; j < NREP; ++j) {
-          dn[j] = group_sum_dpp<LPK>(dotf(qv[j], k2n)) * scale;
+          for (int i = 0; i < 4; ++i) kf[i] = unp(k2n[i]);
 #pragma unroll
-          for (int c = 0; c < IC; ++c) {
-            const float d = group_sum_dpp<LPK>(dotf(qv[j], kq[c])) * scale;
+          for (int j = 0; j < NREP; ++j) dn[j] = group_sum_dpp<LPK>(dot_pk(j, kf)) * scale;
+        }
+#pragma unroll
+        for (int c = 0; c < IC; ++c) {
+          f2v kf[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) kf[i] = unp(kq[c][i]);
+#pragma unroll
+          for (int j = 0; j < NREP; ++j) {
+            const float d = group_sum_dpp<LPK>(dot_pk(j, kf)) * scale;
             dd[j][c] = c * GPW + grp < nc ? d : -INFINITY;
           }
         }
-        float vnf[8];
+        f2v vn2[4], vf[IC][4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) vnf[i] = s.vn[w][sub * 8 + i];
+        for (int i = 0; i < 4; ++i) vn2[i] = f2v{s.vn[w][sub * 8 + 2 * i], s.vn[w][sub * 8 + 2 * i + 1]};
+#pragma unroll
+        for (int c = 0; c < IC; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) vf[c][i] = unp(vq[c][i]);
         float m[NREP], lsum[NREP], o[NREP][8];
 #pragma unroll
         for (int j = 0; j < NREP; ++j) {
@@ -597,14 +616,12 @@ __global__ __launch_bounds__(NT) void cp_step_k(CEP pk) {
             ls += ev[c];
           }
 #pragma unroll
-          for (int d = 0; d < 8; ++d) {
-            float acc = en * vnf[d];
+          for (int i = 0; i < 4; ++i) {  // output dims 2i, 2i + 1
+            f2v acc = f2v{en, en} * vn2[i];
 #pragma unroll
-            for (int c = 0; c < IC; ++c) {
-              const unsigned u = vq[c][d >> 1];
-              acc = fmaf(ev[c], __uint_as_float((d & 1) ? (u & 0xFFFF0000u) : (u << 16)), acc);
-            }
-            o[j][d] = acc;
+            for (int c = 0; c < IC; ++c) acc = f2v{ev[c], ev[c]} * vf[c][i] + acc;
+            o[j][2 * i] = acc.x;
+            o[j][2 * i + 1] = acc.y;
           }
           m[j] = mn; lsum[j] = ls;
         }
