@@ -103,14 +103,17 @@ def test_cp_step_matches_launch_chain(R, pos):
     print(f"\n  R={R} pos={pos}: logits rel-L2 {e:.2e}, max|d| {float((logits - ref).abs().max()):.3g} "
           f"(|ref| max {float(ref.abs().max()):.3g}); argmax agree {(logits.argmax(-1) == ref.argmax(-1)).float().mean():.2f}")
     assert torch.isfinite(logits).all()
-    assert e < 2e-2
+    # measured 5.7e-3 - 6.5e-3 (the engine's attention is fp32, the fused chain's attn_oproj_hs_k rounds q and the
+    # softmax weights to bf16; tests/test_gpu_engine_stages.py pins each against fp64)
+    assert e < 1e-2
     for li in range(st.n_layers):
         # layer 0's new key / value come from the same q/k/v rows: identical; later layers within bf16 rounding
         if li == 0:
             assert torch.equal(kc2[li], kc1[li]) and torch.equal(vc2[li], vc1[li])
         else:
-            assert _rel(kc2[li][:, :, pos], kc1[li][:, :, pos]) < 2e-2
-            assert _rel(vc2[li][:, :, pos], vc1[li][:, :, pos]) < 2e-2
+            ek, ev = _rel(kc2[li][:, :, pos], kc1[li][:, :, pos]), _rel(vc2[li][:, :, pos], vc1[li][:, :, pos])
+            print(f"  layer {li}: new key rel {ek:.2e}, value rel {ev:.2e}")
+            assert ek < 1e-2 and ev < 1e-2
             assert torch.equal(kc2[li][:, :, :pos], kc1[li][:, :, :pos])  # nothing else written
 
 
@@ -130,7 +133,7 @@ def test_cp_step_launch_sequence_on_one_workspace():
                      pos, dev)
         logits = torch.full((R, lm.N), float("nan"), device=dev)
         Kn.cp_step(st.layers, lm, x, qkv0, R, kc, vc, Lmax, pos, st.cos, st.sin, st.eps, logits, ws)
-        assert _rel(logits, ref) < 2e-2, (i, R, pos, _rel(logits, ref))
+        assert _rel(logits, ref) < 1e-2, (i, R, pos, _rel(logits, ref))
     epoch = int(ws[4:8].view(torch.int32).item())
     assert epoch == 17
     assert int(ws[:4].view(torch.int32).item()) == 0
@@ -187,11 +190,12 @@ def test_cp_prefill_matches_launch_chain(R):
     e = _rel(logits, ref)
     print(f"\n  prefill R={R}: logits rel-L2 {e:.2e}; argmax agree {(logits.argmax(-1) == ref.argmax(-1)).float().mean():.2f}")
     assert torch.isfinite(logits).all()
-    assert e < 2e-2
+    assert e < 5e-3  # measured 2.6e-3 - 3.4e-3
     for li in range(st.n_layers):
         for t in range(2):
-            assert _rel(kc2[li][:, :, t], kc1[li][:, :, t]) < 2e-2, (li, t)
-            assert _rel(vc2[li][:, :, t], vc1[li][:, :, t]) < 2e-2, (li, t)
+            ek, ev = _rel(kc2[li][:, :, t], kc1[li][:, :, t]), _rel(vc2[li][:, :, t], vc1[li][:, :, t])
+            print(f"  layer {li} position {t}: key rel {ek:.2e}, value rel {ev:.2e}")
+            assert ek < 5e-3 and ev < 5e-3, (li, t, ek, ev)
         assert torch.equal(kc2[li][:, :, 2:], kc1[li][:, :, 2:])  # nothing else written
         assert torch.equal(vc2[li][:, :, 2:], vc1[li][:, :, 2:])
     assert int(ws[4:8].view(torch.int32).item()) == 4  # 3 prefills + 1 decode step advanced the launch counter

@@ -97,8 +97,8 @@ def test_talker_tail_matches_chain(R, dims):
     xe, qe = outs[0]
     print(f"\n  H={dims[0]} R={R}: x rel {_rel(xe, xr):.3e}, qkv rel {_rel(qe, qr):.3e}")
     assert torch.isfinite(qe).all()
-    assert _rel(xe, xr) < 2e-3
-    assert _rel(qe, qr) < 2e-2
+    assert _rel(xe, xr) < 2e-4  # measured <= 3.6e-5 (summation order; fp32 residual)
+    assert _rel(qe, qr) < 1e-3  # measured <= 2.3e-4 (x16 rounding flips of the bf16 operand)
     for xo, qo in outs[1:]:  # deterministic (fixed reduction orders)
         assert torch.equal(xo, xe) and torch.equal(qo, qe)
 
@@ -123,7 +123,7 @@ def test_talker_tail_last_layer_and_many_launches(dims):
         torch.cuda.synchronize()
         if nxt is None:
             assert bool((qe == 7.0).all())
-            assert _rel(xe, xr) < 2e-3
+            assert _rel(xe, xr) < 2e-4
             if first is None:
                 first = xe
             assert torch.equal(xe, first)
