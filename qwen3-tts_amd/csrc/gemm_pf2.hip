@@ -2,6 +2,7 @@
 // codec pre-transformer linears on bf16 activations), routed here by qt_gemm (gemm.hip) for bf16 A + bf16 pre-tiled
 // weights with K % 64 == 0.  Own translation unit so the tile configurations build in parallel with gemm.hip.
 #include "gemm_p.h"
+#include "engine_dev.h"
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -10,7 +11,8 @@
 __device__ unsigned long long pf2_stamps[1 << 14][4];
 #define PF2_STAMP(k)                                                                            \
   do {                                                                                          \
-    if (threadIdx.x == 0 && blockIdx.x < (1 << 14)) pf2_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && blockIdx.x + blockIdx.y * gridDim.x < (1 << 14))                   \
+      pf2_stamps[blockIdx.x + blockIdx.y * gridDim.x][k] = __builtin_amdgcn_s_memtime();           \
   } while (0)
 #else
 #define PF2_STAMP(k) do { } while (0)
@@ -77,9 +79,24 @@ QT_DEV void static_for(F&& f) {
 // EPI: the epilogue, compile-time for the prefill linears' plain forms (no act / bias / colscale): PF2_STORE,
 // PF2_ADD (residual add), PF2_ADD_OUT2 (+ bf16 shadow), PF2_SWIGLU; PF2_GENERIC reads all of it from GemmP.
 // ABL (measurement only, tools/pf2_probe.hip), bit mask: 1 no MFMA (fragment reads kept live), 2 no loads after the
-// prologue (the rest runs on stale stages), 4 no fragment reads (and no MFMA), 8 no epilogue (accumulators kept live)
+// prologue (the rest runs on stale stages), 4 no fragment reads (and no MFMA), 8 no epilogue (accumulators kept live),
+// 16 (PP) every block reads column tile 0's weights, 32 (PP) every block reads row tile 0's activations
 enum { PF2_GENERIC = -1, PF2_STORE = 0, PF2_ADD = 1, PF2_SWIGLU = 2, PF2_ADD_OUT2 = 3 };
-template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL, int EPI, int ABL = 0, bool SPLIT = false>
+// PP: the ping-pong schedule (8 waves = two groups of 4, WM = 4 x WN = 2: waves 0-3 own rows [0, BM/2), waves 4-7
+// rows [BM/2, BM)).  Group 1 runs one barrier behind group 0, so on every SIMD one wave multiplies while the other
+// group's wave reads its next stage's fragments from LDS and issues DMAs: the MFMA pipe no longer idles through the
+// fragment reads and the barrier of a stage (cdna_hip_programming.md §5 "The 256^2 8-phase template": the staggered
+// wave groups; two phases per 64-deep stage here).  Per stage s (PP = 3, the product form):
+//   group 0:  R(s): issue stage s+NS-1, read stage s's fragments | k=2s   | C(s): MFMAs, wait stage s+1 | k=2s+1
+//   group 1:  (stagger barrier k=0 first)  R(s): read, wait stage s+1 | k=2s+1 | C(s): MFMAs, issue stage s+NS | k=2s+2
+// Stage s is waited for by every wave before barrier 2s-1 (the one before group 0 first reads it); its LDS slot is
+// refilled (stage s+NS) only after barrier 2s+1, which ends group 1's read of it (lgkmcnt(0) before that barrier).
+// PP = 1 issues group 1's stage before its MFMAs instead (measured slower: an LDS-DMA issue costs the issuing wave
+// ~100 cycles, MI355X_MICROARCH.md cycle constants; profiles/r06_pf2_pingpong_probe.txt).
+// The DMA pieces (A_FR + B_FR of 1 KiB) are dealt round-robin over the 8 waves (the first TOT % 8 waves take one
+// more), so tile widths whose fragment count is not a multiple of 8 (BN = 160) work; each wave counts its own.
+template <typename OT, int BM, int NTB, int NS, int WM, int WN, bool AFL, int EPI, int ABL = 0, bool SPLIT = false,
+          int PP = 0>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   constexpr int NW = WM * WN;
   constexpr int MI = BM / WM / 16;            // row fragments per wave
@@ -87,7 +104,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   constexpr int A_FR = BM / 8, B_FR = NTB * 2;  // 1 KiB fragments per stage
   constexpr int STAGE = (A_FR + B_FR) * 512;  // bf16 elements per stage
   constexpr int GA = A_FR / NW, GB = B_FR / NW, G = GA + GB;  // DMA instructions per wave per stage
-  static_assert(A_FR % NW == 0 && B_FR % NW == 0 && MI >= 1 && CT >= 1, "fragments split over the waves");
+  static_assert(PP || (A_FR % NW == 0 && B_FR % NW == 0), "fragments split over the waves");
+  static_assert(MI >= 1 && CT >= 1 && NTB % WN == 0 && BM % (WM * 16) == 0, "wave tiles");
+  static_assert(!PP || (WM == 4 && WN == 2 && AFL && NS >= 2 && (PP == 1 || PP == 3)), "ping-pong: two groups of 2 x 2 waves");
   // NS stages, then the row sums of squares: WN partial sums per row (one per wave of a row block)
   // (one __shared__ object: the split-K arrival flag lives at its end, after the row sums)
   __shared__ __attribute__((aligned(16))) bf16_t smem_pf2[NS * STAGE + 2 * WN * BM + 8];
@@ -149,6 +168,129 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
 #pragma unroll
   for (int i = 0; i < MI; ++i) ss[i] = 0.f;
   const int wj = w % WN;
+  if constexpr (PP) {
+    constexpr int TOT = A_FR + B_FR, GQ = TOT / NW, GR = TOT % NW, GMAX = GQ + (GR ? 1 : 0);
+    const bool extra = w < GR;  // wave-uniform: this wave issues GQ + 1 pieces per stage
+    const int g = w >> 2;
+    auto issue_pp = [&](int ls) {
+      const unsigned sb = lbase + (unsigned)((ls % NS) * STAGE * 2);
+      const int st = s_lo + ls;
+#pragma unroll
+      for (int i = 0; i < GMAX; ++i) {
+        const int f = w + NW * i;
+        if (i < GQ || extra) {
+          if (f < A_FR) {  // full 128-B lines: rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+            const int rr = f * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((rr >> 1) & 7);
+            const int row = (ABL & 32) ? rr : min(m0 + rr, p.M - 1);
+            glds16(Ab + (long long)row * p.lda + st * 64 + c * 8, sb + f * 1024);
+          } else {
+            const int fb = f - A_FR, ct = fb >> 1, kt = fb & 1;
+            const int nt = (ABL & 16) ? ct : min(nt0 + ct, ntl - 1);
+            glds16(Wb + ((size_t)nt * ktiles + st * 2 + kt) * 512 + lane * 8, sb + f * 1024);
+          }
+        }
+      }
+    };
+    // wait until at most `after` stages issued after the awaited one remain in flight (this wave's own DMAs)
+    auto wait_pp = [&](int after) {
+      if (GR && extra) vm_wait_stages<GQ + 1, NS - 1>(after);
+      else vm_wait_stages<GQ, NS - 1>(after);
+    };
+    u32x4_t af[2][MI], bfr[2][CT];
+    auto read_frags = [&](int s, auto&& between) {
+      if constexpr ((ABL & 4) != 0) { between(); return; }
+      const bf16_t* sa = smem_pf2 + (s % NS) * STAGE;
+      const bf16_t* sbf = sa + A_FR * 512;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < CT; ++j) bfr[kk][j] = *(const u32x4_t*)(sbf + ((wc + j) * 2 + kk) * 512 + lane * 8);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          af[kk][i] = *(const u32x4_t*)(sa + (wr + i * 16 + lm) * 64 + (((kk * 4 + lk) ^ (lm >> 1)) * 8));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      between();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto compute = [&]() {
+      if constexpr ((ABL & 4) != 0) return;
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(af[kk][i]));
+#pragma unroll
+          for (int j = 0; j < CT; ++j) asm volatile("" ::"v"(bfr[kk][j]));
+        }
+        return;
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < CT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[kk][i]),
+                                                                __builtin_bit_cast(bf16x8_t, bfr[kk][j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (norm) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int e2 = 0; e2 < 4 / WN; ++e2) {
+              unsigned d = af[kk][i][e2 * WN];
+#pragma unroll
+              for (int t = 1; t < WN; ++t) d = wj == t ? af[kk][i][e2 * WN + t] : d;
+              const bf16x2_t h = __builtin_bit_cast(bf16x2_t, d);
+              ss[i] = __builtin_amdgcn_fdot2_f32_bf16(h, h, ss[i], false);
+            }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto nop = [] {};
+    {
+      // prologue: group 0 stages 0..NS-2 (it issues NS-1 in R(0)), group 1 stages 0..NS-1; stage 0 landed for all
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s)
+        if (s < S) issue_pp(s);
+      if (g == 1 && NS - 1 < S) issue_pp(NS - 1);
+      wait_pp(min(S - 1, g == 0 ? NS - 2 : NS - 1));
+      bar();
+      if (g == 0) {
+        for (int s = 0; s < S; ++s) {
+          if (!(ABL & 2) && s + NS - 1 < S) issue_pp(s + NS - 1);
+          read_frags(s, nop);
+          bar();  // k = 2s
+          compute();
+          if (s + 1 < S) wait_pp(min(S - 1, s + NS - 1) - (s + 1));
+          bar();  // k = 2s + 1
+        }
+        bar();  // group 1's last barrier
+      } else {
+        bar();  // k = 0: the stagger
+        for (int s = 0; s < S; ++s) {
+          read_frags(s, nop);
+          if (s + 1 < S) wait_pp(min(S - 1, s + NS - 1) - (s + 1));
+          bar();  // k = 2s + 1
+          if (PP == 1 && !(ABL & 2) && s + NS < S) issue_pp(s + NS);
+          compute();
+          if (PP == 3 && !(ABL & 2) && s + NS < S) issue_pp(s + NS);
+          bar();  // k = 2s + 2
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < S) issue(s);
@@ -198,6 +340,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
       }
     }
   }
+  }  // !PP
   PF2_STAMP(1);
   if (norm) {  // row sums: lanes l, l^16, l^32, l^48 hold the four k chunks of row l & 15
 #pragma unroll
@@ -209,26 +352,25 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
     __syncthreads();  // (no DMA in flight any more)
   }
   if constexpr (SPLIT) {
-    // deterministic split-K: every split stores its accumulators (and row sums of squares) write-through, one lane
-    // counts the arrival after every storing wave's drain + a barrier, and the last split to arrive sums all splits'
-    // records in split order, then runs the epilogue (MI355X_MICROARCH.md visibility table, first row)
+    // deterministic split-K: every split stores its accumulators (and row sums of squares) write-through (16-byte sc1
+    // buffer stores), one lane counts the arrival after every storing wave's drain + a barrier, and the last split to
+    // arrive sums all splits' records in split order (its own from registers, the others by 16-byte sc1 loads), then
+    // runs the epilogue (MI355X_MICROARCH.md visibility table, first row; cdna_hip_programming.md §5 "Projection GEMM
+    // at M = 256" item 2, the sc1 form)
     constexpr int FR = MI * CT, REC = NW * FR * 256 + WN * BM;  // floats per split record
     int& pf2_last = *(int*)(smem_pf2 + NS * STAGE + 2 * WN * BM);
-    unsigned long long* rec = (unsigned long long*)(p.part + ((size_t)wg * KS + z) * REC);
+    const qt_engine::rsrc_t rr_all = qt_engine::mkr(p.part + (size_t)wg * KS * REC, (unsigned)(KS * REC * 4));
+    const unsigned own = (unsigned)z * REC * 4;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < CT; ++j) {
-        unsigned long long* d = rec + ((w * FR + i * CT + j) * 256 + lane * 4) / 2;
-        __hip_atomic_store(d, __builtin_bit_cast(unsigned long long, (f32x2_t){acc[i][j][0], acc[i][j][1]}),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 1, __builtin_bit_cast(unsigned long long, (f32x2_t){acc[i][j][2], acc[i][j][3]}),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    float* srec = (float*)rec + NW * FR * 256;
+      for (int j = 0; j < CT; ++j)
+        qt_engine::bst4_c(__builtin_bit_cast(u32x4_t, acc[i][j]), rr_all,
+                          own + (unsigned)(((w * FR + i * CT + j) * 256 + lane * 4) * 4));
+    const unsigned sso = (unsigned)(NW * FR * 256) * 4;
     if (norm)
       for (int e = tid; e < WN * BM; e += NW * 64)
-        __hip_atomic_store(srec + e, ss_row[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qt_engine::bst_c(__float_as_uint(ss_row[e]), rr_all, own + sso + e * 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival is counted
     __syncthreads();
     if (tid == 0) {
@@ -238,39 +380,37 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
     }
     __syncthreads();
     if (!pf2_last) return;
-    const unsigned long long* base = (const unsigned long long*)(p.part + (size_t)wg * KS * REC);
+    auto merge = [&](auto KSC) {
+      constexpr int KSN = decltype(KSC)::value;
+      // the other KSN - 1 records (k -> split k + (k >= z)) in flight before the adds; no branch around a load
+      f32x4_t v[KSN - 1][MI][CT];
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int k = 0; k < KSN - 1; ++k)
 #pragma unroll
-      for (int j = 0; j < CT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    f32x2_t v[PF2_KS_MAX][MI][CT][2];  // every split's record in flight before the adds
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int zz = 0; zz < PF2_KS_MAX; ++zz)
+          for (int j = 0; j < CT; ++j)
+            v[k][i][j] = __builtin_bit_cast(f32x4_t, qt_engine::bld_c(rr_all, (unsigned)((k + (k >= z)) * REC * 4) +
+                                                                       (unsigned)(((w * FR + i * CT + j) * 256 + lane * 4) * 4)));
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < CT; ++j) {
-          const unsigned long long* d =
-              base + ((size_t)min(zz, KS - 1) * REC + (w * FR + i * CT + j) * 256 + lane * 4) / 2;
-          v[zz][i][j][0] = __builtin_bit_cast(f32x2_t, __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          v[zz][i][j][1] = __builtin_bit_cast(f32x2_t, __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          f32x4_t t = z == 0 ? acc[i][j] : v[0][i][j];
+#pragma unroll
+          for (int zz = 1; zz < KSN; ++zz)  // split order: split zz is the own partial, v[zz] or v[zz - 1]
+            t += zz == z ? acc[i][j] : (zz < z ? v[zz < KSN - 1 ? zz : KSN - 2][i][j] : v[zz - 1][i][j]);
+          acc[i][j] = t;
         }
-#pragma unroll
-    for (int zz = 0; zz < PF2_KS_MAX; ++zz)  // split order
-      if (zz < KS) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < CT; ++j) {
-            acc[i][j][0] += v[zz][i][j][0][0]; acc[i][j][1] += v[zz][i][j][0][1];
-            acc[i][j][2] += v[zz][i][j][1][0]; acc[i][j][3] += v[zz][i][j][1][1];
-          }
-      }
+    };
+    if (KS == 2) merge(std::integral_constant<int, 2>{});
+    else if (KS == 3) merge(std::integral_constant<int, 3>{});
+    else merge(std::integral_constant<int, PF2_KS_MAX>{});
     if (norm) {
-      const float* sb = (const float*)base + NW * FR * 256;
       for (int e = tid; e < WN * BM; e += NW * 64) {
         float t = 0.f;
-        for (int zz = 0; zz < KS; ++zz) t += __hip_atomic_load(sb + (size_t)zz * REC + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int zz = 0; zz < KS; ++zz)
+          t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr_all, (int)(zz * REC * 4 + sso + e * 4), 0, qt_engine::SC1));
         ss_row[e] = t;
       }
       __syncthreads();
@@ -320,7 +460,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   const bool add = EPI == PF2_GENERIC ? p.epi == QT_EPI_ADD : (EPI == PF2_ADD || EPI == PF2_ADD_OUT2);
   const bool swiglu = EPI == PF2_GENERIC ? p.epi == QT_EPI_SWIGLU : EPI == PF2_SWIGLU;
   // residual rows are loaded RCH row fragments at a time (all of them up to 64 registers)
-  constexpr int RCH = (MI * CT * 4 <= 64) ? MI : (64 / (CT * 4) > 0 ? 64 / (CT * 4) : 1);
+  // (32 registers in the ping-pong kernels: two waves per SIMD, 256 registers each)
+  constexpr int RB = PP ? 32 : 64;
+  constexpr int RCH = (MI * CT * 4 <= RB) ? MI : (RB / (CT * 4) > 0 ? RB / (CT * 4) : 1);
   auto run = [&](auto FULLC) {
     constexpr bool FULL = decltype(FULLC)::value;
     static_for<0, (MI + RCH - 1) / RCH>([&](auto C) {
@@ -408,67 +550,82 @@ int pf2_splits(const GemmP& p, int nwg) {
   return std::max(ks, 1);
 }
 
-template <typename OT, int BM, int NTB, int NS, int WM = 2, int WN = 2, bool AFL = true>
-void launch_pf2(const GemmP& p, hipStream_t s) {
+template <typename OT, int BM, int NTB, int NS, int WM = 2, int WN = 2, bool AFL = true, int PP = 0>
+void launch_pf2(const GemmP& p, hipStream_t s, int ks_pp = 1) {
   const int ntl = (p.N + 15) / 16;
   const int nwg = ((p.M + BM - 1) / BM) * ((ntl + NTB - 1) / NTB);
-  const int ks = BM <= 128 ? pf2_splits<BM, NTB, WM, WN>(p, nwg) : 1;
+  const int ks = PP ? ks_pp : (BM <= 128 ? pf2_splits<BM, NTB, WM, WN>(p, nwg) : 1);
   const dim3 g(nwg, ks), b(WM * WN * 64);
   const bool plain = p.act == QT_ACT_NONE && p.bias == nullptr && p.colscale == nullptr;
   if constexpr (BM <= 128) {
     if (ks > 1) {  // narrow outputs: the split instantiations
       if constexpr (std::is_same<OT, bf16_t>::value) {
         if (plain && p.epi == QT_EPI_SWIGLU)
-          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU, 0, true>), g, b, 0, s, p); return; }
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU, 0, true, PP>), g, b, 0, s, p); return; }
       } else {
         if (plain && p.epi == QT_EPI_STORE && !p.out2)
-          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE, 0, true>), g, b, 0, s, p); return; }
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE, 0, true, PP>), g, b, 0, s, p); return; }
         if (plain && p.epi == QT_EPI_ADD && !p.out2)
-          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD, 0, true>), g, b, 0, s, p); return; }
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD, 0, true, PP>), g, b, 0, s, p); return; }
         if (plain && p.epi == QT_EPI_ADD && p.out2)
-          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2, 0, true>), g, b, 0, s, p); return; }
+          { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2, 0, true, PP>), g, b, 0, s, p); return; }
       }
-      hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC, 0, true>), g, b, 0, s, p);
+      hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC, 0, true, PP>), g, b, 0, s, p);
       return;
     }
   }
   if constexpr (std::is_same<OT, bf16_t>::value) {
-    if (plain && p.epi == QT_EPI_SWIGLU) { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU>), g, b, 0, s, p); return; }
+    if (plain && p.epi == QT_EPI_SWIGLU)
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_SWIGLU, 0, false, PP>), g, b, 0, s, p); return; }
   } else {
     if (plain && p.epi == QT_EPI_STORE && !p.out2)
-      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE>), g, b, 0, s, p); return; }
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_STORE, 0, false, PP>), g, b, 0, s, p); return; }
     if (plain && p.epi == QT_EPI_ADD && !p.out2)
-      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD>), g, b, 0, s, p); return; }
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD, 0, false, PP>), g, b, 0, s, p); return; }
     if (plain && p.epi == QT_EPI_ADD && p.out2)
-      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2>), g, b, 0, s, p); return; }
+      { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_ADD_OUT2, 0, false, PP>), g, b, 0, s, p); return; }
   }
-  hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC>), g, b, 0, s, p);
+  hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, AFL, PF2_GENERIC, 0, false, PP>), g, b, 0, s, p);
 }
 
 #ifndef QT_PF2_PROBE
-// Tile configuration (QT_PF2_CFG = 3 / 4 / 9 / 11 forces one, measurement; 0 = chosen by shape).
+// Tile configuration (QT_PF2_CFG = 3 / 4 / 9 / 11 / 21 / 22 forces one, measurement; 0 = chosen by shape).
 // tools/pf2_probe.hip timed every configuration on the 1.7B / 0.6B talker prefill shapes at M = 256 ... 4096
-// (profiles/r03_pf2_probe_sweep.txt): a block's time is nearly independent of M and N (its loop runs K / 64 stages of a
-// fixed tile), so launch time ~ ceil(blocks / resident slots) x block time, and the best tile is the one whose
-// block count quantises best onto the 256 CUs.  Block cycles per 2048 of K and epilogue cycles below are those
-// measurements; cfg 3 (72 KiB of LDS) runs 2 blocks per CU, the others 1.
-struct Pf2Cfg { int id, BM, BN, bpc; float loop1, loop2, epi; };
+// (profiles/r03_pf2_probe_sweep.txt, profiles/r06_pf2_pingpong_probe.txt): a block's time is nearly independent of M
+// and N (its loop runs K / 64 stages of a fixed tile), so launch time ~ ceil(blocks / resident slots) x block time,
+// and the best tile is the one whose block count quantises best onto the 256 CUs.  Block cycles per 2048 of K and
+// epilogue cycles below are those measurements; cfg 3 (72 KiB of LDS) runs 2 blocks per CU, the others 1.  The
+// ping-pong configurations (pp, 8 waves in two staggered groups) are considered from 256 rows (long prefills: voice
+// clone, non-streaming prompts); cfg 22 is cfg 21 with K split over two blocks (per-block K in its loop figure, its
+// epilogue the record merge), only for <= 2048-column outputs whose two-fold grid fits the 256 CUs.
+struct Pf2Cfg { int id, BM, BN, bpc; float loop1, loop2, epi; int pp, ks; };
 constexpr Pf2Cfg PF2_CFGS[] = {
-    {3, 128, 64, 2, 31000.f, 44000.f, 4000.f},   // 4 waves, wave tile 64 x 32
-    {11, 64, 96, 1, 28000.f, 28000.f, 3000.f},   // 4 waves, wave tile 32 x 48
-    {4, 256, 128, 1, 68000.f, 68000.f, 8000.f},  // 8 waves, wave tile 64 x 64
-    {9, 256, 160, 1, 95000.f, 95000.f, 10000.f}, // 4 waves, wave tile 128 x 80
+    {3, 128, 64, 2, 31000.f, 44000.f, 4000.f, 0, 1},   // 4 waves, wave tile 64 x 32
+    {11, 64, 96, 1, 28000.f, 28000.f, 3000.f, 0, 1},   // 4 waves, wave tile 32 x 48
+    {4, 256, 128, 1, 68000.f, 68000.f, 8000.f, 0, 1},  // 8 waves, wave tile 64 x 64
+    {9, 256, 160, 1, 76500.f, 76500.f, 9000.f, 1, 1},  // ping-pong, 8 waves, wave tile 64 x 80 (4-wave form: 95000)
+    {21, 128, 128, 1, 42600.f, 42600.f, 2500.f, 1, 1}, // ping-pong, 8 waves, wave tile 32 x 64
+    {22, 128, 128, 1, 45000.f, 45000.f, 9500.f, 1, 2}, // cfg 21, split-K 2
 };
 inline int pf2_cfg_env() {
   static const int v = qt_knob("QT_PF2_CFG", 0);
   return v;
 }
-inline int pf2_pick(int M, int N, int K) {
+inline bool pf2_split_fits(const GemmP& p, long long tiles, int ks) {  // cfg 22's records in the caller's workspace
+  constexpr long long rec = 8ll * 2 * 4 * 256 + 2 * 128;  // NW x MI x CT x 256 + WN x BM floats
+  return p.part != nullptr && p.cnt != nullptr && tiles <= 4096 && tiles * ks * rec * 4 <= p.part_bytes;
+}
+inline int pf2_pick(const GemmP& p) {
+  static const int pp_env = qt_knob("QT_PF2_PP", 1);  // 0: without the ping-pong configurations (A/B)
+  const int M = p.M, N = p.N, K = p.Klog;
   int best = 3;
   float best_t = 3.4e38f;
   for (const Pf2Cfg& c : PF2_CFGS) {
-    const long long blocks = (long long)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
-    const float kf = K / 2048.f;
+    if (c.pp && (M < 256 || !pp_env)) continue;
+    const long long tiles = (long long)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
+    if (c.ks > 1 && (N > 2048 || tiles * c.ks > 256 || K / 64 < 32 || !pf2_split_fits(p, tiles, c.ks))) continue;
+    const long long blocks = tiles * c.ks;
+    const float kf = K / 2048.f / c.ks;
     float t;
     if (c.bpc == 2 && blocks > 256) t = (float)((blocks + 511) / 512) * (c.loop2 * kf + c.epi);
     else t = (float)((blocks + 255) / 256) * (c.loop1 * kf + c.epi);
@@ -480,12 +637,15 @@ inline int pf2_pick(int M, int N, int K) {
 template <typename OT>
 void launch_pf2_auto(const GemmP& p, hipStream_t s) {
   int cfg = pf2_cfg_env();
-  if (cfg == 0) cfg = pf2_pick(p.M, p.N, p.Klog);
+  if (cfg == 0) cfg = pf2_pick(p);
+  if (cfg == 22 && !pf2_split_fits(p, (long long)((p.M + 127) / 128) * ((p.N + 127) / 128), 2)) cfg = 21;
   // (deeper pipelines of the two small-tile configurations -- 7 stages of 64 x 96, 6 of 128 x 64, one block per CU --
   // measured slower at 24..680 rows: gate-up 160 rows 25.4 -> 37.9 us, qkv 680 rows 26.2 -> 37.1;
   // profiles/r04_pf2_deep_ab.txt)
   if (cfg == 4) launch_pf2<OT, 256, 8, 3, 4, 2>(p, s);
-  else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 2, 2>(p, s);
+  else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 4, 2, true, 3>(p, s);
+  else if (cfg == 21) launch_pf2<OT, 128, 8, 4, 4, 2, true, 3>(p, s);
+  else if (cfg == 22) launch_pf2<OT, 128, 8, 4, 4, 2, true, 3>(p, s, 2);
   else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);
   else launch_pf2<OT, 128, 4, 3>(p, s);
 }

@@ -255,17 +255,21 @@ def test_igemm_linear_rms_swiglu_bf16(M, H, I):
 
 
 @pytest.mark.parametrize("M,N,K,mode", [
-    (2900, 3072, 512, "swiglu"), (2900, 3072, 512, "rms"), (650, 11856, 512, "swiglu"),   # 256 x 160, 4 waves
-    (520, 8192, 1024, "rms"), (520, 8192, 1024, "add"), (1100, 4096, 512, "rms"),          # 256 x 128, 8 waves
-    (300, 1000, 640, "add"), (300, 1008, 640, "swiglu"), (131, 2048, 6144, "add_plain"),   # 64 x 96, 4 waves
+    (2900, 3072, 512, "swiglu"), (2900, 3072, 512, "rms"), (650, 11856, 512, "swiglu"),   # cfg 9: 256 x 160 ping-pong
+    (680, 12288, 2048, "swiglu"), (700, 11000, 512, "add"),
+    (520, 8192, 1024, "rms"), (520, 8192, 1024, "add"), (1100, 4096, 512, "rms"),          # cfg 4: 256 x 128, 8 waves
+    (300, 1000, 640, "add"), (300, 1008, 640, "swiglu"), (131, 2048, 6144, "add_plain"),   # cfg 11: 64 x 96, 4 waves
     (680, 2048, 2048, "add_noshadow"),
-    (1300, 2048, 1024, "add"), (1300, 2048, 1024, "add_plain"), (1300, 2056, 1024, "add_noshadow")])  # 128 x 64
+    (1000, 2048, 512, "add"), (1000, 2056, 512, "add_noshadow"),                           # cfg 3: 128 x 64
+    (1300, 2048, 1024, "add"), (1300, 2048, 1024, "add_plain"), (1300, 2056, 1024, "add_noshadow"),  # cfg 21:
+    (680, 4096, 2048, "rms"), (333, 6160, 1024, "swiglu"), (1300, 2048, 512, "add")])       #   128 x 128 ping-pong
 def test_prefill_gemm_pf2_bf16(M, N, K, mode):
     """Deep-pipelined prefill GEMM (gemm_pf2_k: LDS-DMA operands, NS stages in flight) on bf16 A, every tile
-    configuration the shape rule picks (256 x 160 / 4 waves, 256 x 128 / 8 waves, 64 x 96 / 4 waves, 128 x 64 /
-    4 waves; comments above), interior and ragged row / column tiles, every epilogue form: RMSNorm rows from the bf16
-    A values (plain store), SwiGLU, residual add with bias (generic form), without bias with / without the bf16
-    shadow (out2) -- vs torch fp32 on the same bf16-rounded operands."""
+    configuration the shape rule picks (gemm_pf2.hip pf2_pick: 256 x 160 and 128 x 128 ping-pong -- two staggered
+    groups of 4 waves --, 256 x 128 / 8 waves, 64 x 96 / 4 waves, 128 x 64 / 4 waves), interior and ragged row /
+    column tiles, every epilogue form: RMSNorm rows from the bf16 A values (plain store), SwiGLU, residual add with
+    bias (generic form), without bias with / without the bf16 shadow (out2) -- vs torch fp32 on the same bf16-rounded
+    operands."""
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
     g = torch.Generator().manual_seed(M + N + K)
@@ -304,11 +308,14 @@ def test_prefill_gemm_pf2_bf16(M, N, K, mode):
 
 
 @pytest.mark.parametrize("M,N,K,mode", [(200, 2048, 6144, "add"), (200, 2048, 2048, "add_shadow"),
-                                        (300, 1024, 3072, "rms"), (256, 1000, 2048, "add"), (700, 2048, 6144, "add")])
+                                        (300, 1024, 3072, "rms"), (256, 1000, 2048, "add"), (700, 2048, 6144, "add"),
+                                        (680, 2048, 6144, "add_shadow"), (680, 1040, 3072, "rms"),
+                                        (400, 2048, 4096, "add")])
 def test_prefill_gemm_pf2_splitk(M, N, K, mode):
-    """gemm_pf2_k split-K (narrow outputs whose tiles leave most CUs idle: K split over up to 4 blocks per tile, the
-    last split to arrive sums every split's record in split order): matches the unsplit kernel (splitk=1) to fp32
-    rounding and torch fp32, is bitwise reproducible, keeps the RMS rows / residual / bf16 shadow epilogues."""
+    """gemm_pf2_k split-K (narrow outputs whose tiles leave most CUs idle: K split over up to 4 blocks per tile of
+    the 4-wave kernels, over 2 per 128 x 128 ping-pong tile from 256 rows (cfg 22); the last split to arrive sums every
+    split's record in split order): matches the unsplit kernel (splitk=1) to fp32 rounding and torch fp32, is bitwise
+    reproducible, keeps the RMS rows / residual / bf16 shadow epilogues."""
     from qwen_tts import kernels as Kn, _hip
     dev = _dev()
     Kn.gemm_workspace(dev)

@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <vector>
 #include <string>
+#include <cstring>
+#include <cmath>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -30,22 +32,56 @@ __global__ void clock_k(unsigned long long* o) {
   }
 }
 
-template <typename OT, int BM, int NTB, int NS, int WM, int WN, int EPI, int ABL = 0>
+static std::vector<unsigned char> g_ref;
+static double g_relerr = 0;
+static unsigned* g_cnt = nullptr;
+static float* g_part = nullptr;
+constexpr long long PART_BYTES = 64ll << 20;
+template <typename OT, int BM, int NTB, int NS, int WM, int WN, int EPI, int ABL = 0, int PP = 0, int KS = 1>
 void run(const char* name, GemmP p, int reps) {
+  if (!g_cnt) {
+    CK(hipMalloc(&g_cnt, 4096 * 4)); CK(hipMemset(g_cnt, 0, 4096 * 4));
+    CK(hipMalloc(&g_part, PART_BYTES));
+  }
+  p.cnt = g_cnt; p.part = g_part; p.part_bytes = PART_BYTES;
+  {  // the split records must fit the partial buffer (and the counters their array)
+    constexpr long long REC = 8ll * (BM / WM / 16) * (NTB / WN) * 256 + WN * BM;
+    const long long tiles = (long long)((p.M + BM - 1) / BM) * (((p.N + 15) / 16 + NTB - 1) / NTB);
+    if (KS > 1 && (tiles * KS * REC * 4 > PART_BYTES || tiles > 4096)) { printf("%-28s skipped (records)\n", name); return; }
+  }
   const int ntl = (p.N + 15) / 16;
   const int nwg = ((p.M + BM - 1) / BM) * ((ntl + NTB - 1) / NTB);
-  auto go = [&] { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, true, EPI, ABL>), dim3(nwg), dim3(WM * WN * 64), 0, 0, p); };
+  auto go = [&] { hipLaunchKernelGGL((gemm_pf2_k<OT, BM, NTB, NS, WM, WN, true, EPI, ABL, (KS > 1), PP>), dim3(nwg, KS), dim3(WM * WN * 64), 0, 0, p); };
+  // one launch on a zeroed output, compared bit for bit with the first configuration's (same per-element k order)
+  const size_t obytes = (size_t)p.M * p.ldo * sizeof(OT);
+  CK(hipMemset(p.out, 0, obytes));
+  go();
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned char> mine(obytes);
+  CK(hipMemcpy(mine.data(), p.out, obytes, hipMemcpyDeviceToHost));
+  size_t diff = 0;
+  if (g_ref.size() != obytes) g_ref = mine;
+  else for (size_t i = 0; i < obytes; i += sizeof(OT)) diff += memcmp(&mine[i], &g_ref[i], sizeof(OT)) != 0;
+  double maxd = 0, maxr = 0;
+  for (size_t i = 0; i < obytes; i += sizeof(OT)) {
+    float a, b;
+    if constexpr (sizeof(OT) == 4) { memcpy(&a, &mine[i], 4); memcpy(&b, &g_ref[i], 4); }
+    else { unsigned ua = (unsigned)(*(unsigned short*)&mine[i]) << 16, ub = (unsigned)(*(unsigned short*)&g_ref[i]) << 16;
+           memcpy(&a, &ua, 4); memcpy(&b, &ub, 4); }
+    maxd = std::max(maxd, (double)fabsf(a - b)); maxr = std::max(maxr, (double)fabsf(b));
+  }
+  g_relerr = maxd / std::max(maxr, 1e-30);
   for (int i = 0; i < 20; ++i) go();
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
   for (int i = 0; i < reps; ++i) go();
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  std::vector<unsigned long long> st((size_t)nwg * 4);
+  std::vector<unsigned long long> st((size_t)nwg * KS * 4);
   CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(pf2_stamps), st.size() * 8));
   std::vector<double> loop, epi, life;
   unsigned long long t_min = ~0ull, t_max = 0;
-  for (int b = 0; b < nwg; ++b) {
+  for (int b = 0; b < nwg * KS; ++b) {
     loop.push_back((double)(st[b * 4 + 1] - st[b * 4 + 0]));
     const unsigned long long t2 = (ABL & 8) ? st[b * 4 + 1] : st[b * 4 + 2];
     epi.push_back((double)(t2 - st[b * 4 + 1]));
@@ -57,8 +93,8 @@ void run(const char* name, GemmP p, int reps) {
   const double us = 1e3 * ms / reps;
   const double fl = 2.0 * p.M * p.N * (double)p.Klog;
   (void)span;
-  printf("%-28s %5d blocks  %8.1f us  %7.1f TF/s | block median: loop %7.0f cyc  epilogue %6.0f cyc\n",
-         name, nwg, us, fl / us / 1e6, med(loop), med(epi));
+  printf("%-28s %5d blocks x%d  %8.1f us  %7.1f TF/s | block median: loop %7.0f cyc  epilogue %6.0f cyc | %zu differ, max rel %.2e\n",
+         name, nwg, KS, us, fl / us / 1e6, med(loop), med(epi), diff, g_relerr);
 }
 
 struct Shape { int M, N, K, epi, rms; };
@@ -71,6 +107,13 @@ void sweep(GemmP p, int reps) {
   run<OT, 128, 8, 4, 2, 2, E>("cfg13 128x128 4w", p, reps);
   run<OT, 64, 6, 4, 2, 2, E>("cfg11 64x96 4w", p, reps);
   run<OT, 256, 10, 3, 2, 2, E>("cfg9 256x160 4w", p, reps);
+  run<OT, 256, 10, 3, 4, 2, E, 0, 1>("pp1 256x160 (cfg 9 form 1)", p, reps);
+  run<OT, 256, 10, 3, 4, 2, E, 0, 3>("pp3 256x160 (cfg 9)", p, reps);
+  run<OT, 128, 8, 4, 4, 2, E, 0, 1>("pp1 128x128", p, reps);
+  run<OT, 128, 8, 4, 4, 2, E, 0, 3>("pp3 128x128 (cfg 21)", p, reps);
+  run<OT, 128, 8, 4, 4, 2, E, 0, 3, 2>("pp3 128x128 ks2 (cfg 22)", p, reps);
+  run<OT, 64, 6, 6, 4, 2, E, 0, 3>("pp3 64x96 ns6", p, reps);
+  run<OT, 256, 16, 2, 4, 2, E, 0, 3>("pp3 256x256 ns2", p, reps);
 }
 
 int main(int argc, char** argv) {
@@ -99,6 +142,7 @@ int main(int argc, char** argv) {
     p.M = sh.M; p.N = sh.N; p.Kp = sh.K; p.Klog = sh.K; p.A = A; p.lda = sh.K; p.W = W; p.eps = 1e-6f; p.rms = sh.rms;
     p.act = QT_ACT_NONE; p.epi = sh.epi; p.out = out; p.ldo = sh.epi == QT_EPI_SWIGLU ? sh.N / 2 : sh.N; p.ks = 1;
     printf("M=%d N=%d K=%d epi=%d rms=%d\n", sh.M, sh.N, sh.K, sh.epi, sh.rms);
+    g_ref.clear();
     if (abl) {
       if (sh.epi == QT_EPI_SWIGLU) {
         constexpr int E = PF2_SWIGLU;
