@@ -133,29 +133,36 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
   // this lane's DMA sources: A fragment f = w * GA + i covers rows (f >> 1) * 16.., k tile f & 1
   const int arow = min(m0 + lm, p.M - 1);
   const unsigned lbase = lds_u32(smem_pf2);
+  // this lane's DMA sources at the split's first stage, computed once (row clamp, swizzle, 64-bit address math);
+  // a stage advances an A piece by 64 k (128 B) and a B piece by two fragments (2 KiB)
+  const bf16_t* asrc[GA > 0 ? GA : 1];
+  const bf16_t* bsrc[GB > 0 ? GB : 1];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int f = w * GA + i;
+    if constexpr (AFL) {  // full 128-B lines: piece f = rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+      const int rr = f * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((rr >> 1) & 7);
+      const int row = min(m0 + rr, p.M - 1);
+      asrc[i] = Ab + (long long)row * p.lda + s_lo * 64 + c * 8;
+    } else {  // MFMA fragment order: 16 rows x 64 B per piece
+      const int mt = f >> 1, kt = f & 1;
+      const int row = min(arow + mt * 16, p.M - 1);
+      asrc[i] = Ab + (long long)row * p.lda + s_lo * 64 + kt * 32 + lk * 8;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int f = w * GB + i, ct = f >> 1, kt = f & 1;
+    const int nt = min(nt0 + ct, ntl - 1);
+    bsrc[i] = Wb + ((size_t)nt * ktiles + s_lo * 2 + kt) * 512 + lane * 8;
+  }
   auto issue = [&](int ls) {  // local stage ls of this split: LDS buffer ls % NS, k offset of global stage s_lo + ls
     const unsigned sb = lbase + (unsigned)((ls % NS) * STAGE * 2);
-    const int st = s_lo + ls;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int f = w * GA + i;
-      if constexpr (AFL) {  // full 128-B lines: piece f = rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
-        const int rr = f * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((rr >> 1) & 7);
-        const int row = min(m0 + rr, p.M - 1);
-        glds16(Ab + (long long)row * p.lda + st * 64 + c * 8, sb + f * 1024);
-      } else {  // MFMA fragment order: 16 rows x 64 B per piece
-        const int mt = f >> 1, kt = f & 1;
-        const int row = min(arow + mt * 16, p.M - 1);
-        glds16(Ab + (long long)row * p.lda + st * 64 + kt * 32 + lk * 8, sb + f * 1024);
-      }
-    }
+    for (int i = 0; i < GA; ++i) glds16(asrc[i] + ls * 64, sb + (w * GA + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < GB; ++i) {
-      const int f = w * GB + i, ct = f >> 1, kt = f & 1;
-      const int nt = min(nt0 + ct, ntl - 1);
-      glds16(Wb + ((size_t)nt * ktiles + st * 2 + kt) * 512 + lane * 8, sb + (A_FR + f) * 1024);
-    }
+    for (int i = 0; i < GB; ++i) glds16(bsrc[i] + ls * 1024, sb + (A_FR + w * GB + i) * 1024);
   };
   f32x4_t acc[MI][CT];
 #pragma unroll
@@ -172,25 +179,30 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_pf2_k(GemmP p) {
     constexpr int TOT = A_FR + B_FR, GQ = TOT / NW, GR = TOT % NW, GMAX = GQ + (GR ? 1 : 0);
     const bool extra = w < GR;  // wave-uniform: this wave issues GQ + 1 pieces per stage
     const int g = w >> 2;
+    // this lane's source of each of its pieces at the split's first stage (row clamp, swizzle and 64-bit address math
+    // once, not per stage) and the piece's advance per stage: 64 k of an A row (128 B) or two B fragments (2 KiB)
+    const bf16_t* gsrc[GMAX];
+    bool isa[GMAX];
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) {
+      const int f = min(w + NW * i, A_FR + B_FR - 1);
+      isa[i] = f < A_FR;
+      if (isa[i]) {  // full 128-B lines: rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+        const int rr = f * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((rr >> 1) & 7);
+        const int row = (ABL & 32) ? rr : min(m0 + rr, p.M - 1);
+        gsrc[i] = Ab + (long long)row * p.lda + s_lo * 64 + c * 8;
+      } else {
+        const int fb = f - A_FR, ct = fb >> 1, kt = fb & 1;
+        const int nt = (ABL & 16) ? ct : min(nt0 + ct, ntl - 1);
+        gsrc[i] = Wb + ((size_t)nt * ktiles + s_lo * 2 + kt) * 512 + lane * 8;
+      }
+    }
     auto issue_pp = [&](int ls) {
       const unsigned sb = lbase + (unsigned)((ls % NS) * STAGE * 2);
-      const int st = s_lo + ls;
 #pragma unroll
-      for (int i = 0; i < GMAX; ++i) {
-        const int f = w + NW * i;
-        if (i < GQ || extra) {
-          if (f < A_FR) {  // full 128-B lines: rows 8f..8f+7 x 64 k, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
-            const int rr = f * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((rr >> 1) & 7);
-            const int row = (ABL & 32) ? rr : min(m0 + rr, p.M - 1);
-            glds16(Ab + (long long)row * p.lda + st * 64 + c * 8, sb + f * 1024);
-          } else {
-            const int fb = f - A_FR, ct = fb >> 1, kt = fb & 1;
-            const int nt = (ABL & 16) ? ct : min(nt0 + ct, ntl - 1);
-            glds16(Wb + ((size_t)nt * ktiles + st * 2 + kt) * 512 + lane * 8, sb + f * 1024);
-          }
-        }
-      }
+      for (int i = 0; i < GMAX; ++i)
+        if (i < GQ || extra) glds16(gsrc[i] + (isa[i] ? ls * 64 : ls * 1024), sb + (w + NW * i) * 1024);
     };
     // wait until at most `after` stages issued after the awaited one remain in flight (this wave's own DMAs)
     auto wait_pp = [&](int after) {
