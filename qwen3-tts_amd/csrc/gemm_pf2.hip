@@ -601,7 +601,7 @@ void launch_pf2(const GemmP& p, hipStream_t s, int ks_pp = 1) {
 }
 
 #ifndef QT_PF2_PROBE
-// Tile configuration (QT_PF2_CFG = 3 / 4 / 9 / 11 / 21 / 22 forces one, measurement; 0 = chosen by shape).
+// Tile configuration (QT_PF2_CFG = 3 / 4 / 9 / 11 / 21 / 22 / 23 forces one, measurement; 0 = chosen by shape).
 // tools/pf2_probe.hip timed every configuration on the 1.7B / 0.6B talker prefill shapes at M = 256 ... 4096
 // (profiles/r03_pf2_probe_sweep.txt, profiles/r06_pf2_pingpong_probe.txt): a block's time is nearly independent of M
 // and N (its loop runs K / 64 stages of a fixed tile), so launch time ~ ceil(blocks / resident slots) x block time,
@@ -618,6 +618,7 @@ constexpr Pf2Cfg PF2_CFGS[] = {
     {9, 256, 160, 1, 76500.f, 76500.f, 9000.f, 1, 1},  // ping-pong, 8 waves, wave tile 64 x 80 (4-wave form: 95000)
     {21, 128, 128, 1, 42600.f, 42600.f, 2500.f, 1, 1}, // ping-pong, 8 waves, wave tile 32 x 64
     {22, 128, 128, 1, 45000.f, 45000.f, 9500.f, 1, 2}, // cfg 21, split-K 2
+    {23, 256, 256, 1, 97500.f, 97500.f, 10000.f, 1, 1}, // ping-pong, 8 waves, wave tile 64 x 128, 2 LDS stages
 };
 inline int pf2_cfg_env() {
   static const int v = qt_knob("QT_PF2_CFG", 0);
@@ -658,6 +659,7 @@ void launch_pf2_auto(const GemmP& p, hipStream_t s) {
   else if (cfg == 9) launch_pf2<OT, 256, 10, 3, 4, 2, true, 3>(p, s);
   else if (cfg == 21) launch_pf2<OT, 128, 8, 4, 4, 2, true, 3>(p, s);
   else if (cfg == 22) launch_pf2<OT, 128, 8, 4, 4, 2, true, 3>(p, s, 2);
+  else if (cfg == 23) launch_pf2<OT, 256, 16, 2, 4, 2, true, 3>(p, s);
   else if (cfg == 11) launch_pf2<OT, 64, 6, 4, 2, 2>(p, s);
   else launch_pf2<OT, 128, 4, 3>(p, s);
 }

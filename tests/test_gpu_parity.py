@@ -262,10 +262,11 @@ def test_igemm_linear_rms_swiglu_bf16(M, H, I):
     (680, 2048, 2048, "add_noshadow"),
     (1000, 2048, 512, "add"), (1000, 2056, 512, "add_noshadow"),                           # cfg 3: 128 x 64
     (1300, 2048, 1024, "add"), (1300, 2048, 1024, "add_plain"), (1300, 2056, 1024, "add_noshadow"),  # cfg 21:
-    (680, 4096, 2048, "rms"), (333, 6160, 1024, "swiglu"), (1300, 2048, 512, "add")])       #   128 x 128 ping-pong
+    (680, 4096, 2048, "rms"), (333, 6160, 1024, "swiglu"), (1300, 2048, 512, "add"),       #   128 x 128 ping-pong
+    (1536, 8192, 1024, "swiglu"), (1700, 8190, 1024, "rms"), (2900, 4096, 1024, "add_noshadow")])  # cfg 23: 256 x 256
 def test_prefill_gemm_pf2_bf16(M, N, K, mode):
     """Deep-pipelined prefill GEMM (gemm_pf2_k: LDS-DMA operands, NS stages in flight) on bf16 A, every tile
-    configuration the shape rule picks (gemm_pf2.hip pf2_pick: 256 x 160 and 128 x 128 ping-pong -- two staggered
+    configuration the shape rule picks (gemm_pf2.hip pf2_pick: 256 x 256, 256 x 160 and 128 x 128 ping-pong -- two staggered
     groups of 4 waves --, 256 x 128 / 8 waves, 64 x 96 / 4 waves, 128 x 64 / 4 waves), interior and ragged row /
     column tiles, every epilogue form: RMSNorm rows from the bf16 A values (plain store), SwiGLU, residual add with
     bias (generic form), without bias with / without the bf16 shadow (out2) -- vs torch fp32 on the same bf16-rounded
