@@ -263,7 +263,10 @@ def test_igemm_linear_rms_swiglu_bf16(M, H, I):
     (1000, 2048, 512, "add"), (1000, 2056, 512, "add_noshadow"),                           # cfg 3: 128 x 64
     (1300, 2048, 1024, "add"), (1300, 2048, 1024, "add_plain"), (1300, 2056, 1024, "add_noshadow"),  # cfg 21:
     (680, 4096, 2048, "rms"), (333, 6160, 1024, "swiglu"), (1300, 2048, 512, "add"),       #   128 x 128 ping-pong
-    (1536, 8192, 1024, "swiglu"), (1700, 8190, 1024, "rms"), (2900, 4096, 1024, "add_noshadow")])  # cfg 23: 256 x 256
+    (1536, 8192, 1024, "swiglu"), (1700, 8190, 1024, "rms"), (2900, 4096, 1024, "add_noshadow"),  # cfg 23: 256 x 256
+    # ping-pong with 1..3 K stages (the two groups' prologue / stagger / drain with fewer stages than LDS slots)
+    (300, 4096, 64, "rms"), (680, 4096, 192, "add"), (700, 12288, 64, "swiglu"), (700, 12288, 192, "swiglu"),
+    (1600, 8192, 128, "rms"), (3000, 8192, 192, "add_noshadow")])
 def test_prefill_gemm_pf2_bf16(M, N, K, mode):
     """Deep-pipelined prefill GEMM (gemm_pf2_k: LDS-DMA operands, NS stages in flight) on bf16 A, every tile
     configuration the shape rule picks (gemm_pf2.hip pf2_pick: 256 x 256, 256 x 160 and 128 x 128 ping-pong -- two staggered
@@ -311,7 +314,7 @@ def test_prefill_gemm_pf2_bf16(M, N, K, mode):
 @pytest.mark.parametrize("M,N,K,mode", [(200, 2048, 6144, "add"), (200, 2048, 2048, "add_shadow"),
                                         (300, 1024, 3072, "rms"), (256, 1000, 2048, "add"), (700, 2048, 6144, "add"),
                                         (680, 2048, 6144, "add_shadow"), (680, 1040, 3072, "rms"),
-                                        (400, 2048, 4096, "add")])
+                                        (400, 2048, 4096, "add"), (700, 2048, 4160, "add")])
 def test_prefill_gemm_pf2_splitk(M, N, K, mode):
     """gemm_pf2_k split-K (narrow outputs whose tiles leave most CUs idle: K split over up to 4 blocks per tile of
     the 4-wave kernels, over 2 per 128 x 128 ping-pong tile from 256 rows (cfg 22); the last split to arrive sums every
