@@ -107,11 +107,10 @@ void sweep(GemmP p, int reps) {
   run<OT, 128, 8, 4, 2, 2, E>("cfg13 128x128 4w", p, reps);
   run<OT, 64, 6, 4, 2, 2, E>("cfg11 64x96 4w", p, reps);
   run<OT, 256, 10, 3, 2, 2, E>("cfg9 256x160 4w", p, reps);
-  run<OT, 256, 10, 3, 4, 2, E, 0, 3>("pp3 256x160 (cfg 9)", p, reps);
-  run<OT, 128, 8, 4, 4, 2, E, 0, 3>("pp3 128x128 (cfg 21)", p, reps);
-  run<OT, 256, 16, 2, 4, 2, E, 0, 3>("pp3 256x256 ns2 (cfg 23)", p, reps);
-  run<OT, 256, 8, 3, 4, 2, E, 0, 3>("pp3 256x128 ns3", p, reps);
-  run<OT, 256, 12, 2, 4, 2, E, 0, 3>("pp3 256x192 ns2", p, reps);
+  run<OT, 64, 6, 4, 2, 2, E, 0, 0, 2>("cfg11 ks2", p, reps);
+  run<OT, 64, 6, 4, 2, 2, E, 0, 0, 3>("cfg11 ks3", p, reps);
+  run<OT, 128, 4, 3, 2, 2, E, 0, 0, 2>("cfg3 ks2", p, reps);
+  run<OT, 128, 4, 3, 2, 2, E, 0, 0, 4>("cfg3 ks4", p, reps);
 }
 
 int main(int argc, char** argv) {
