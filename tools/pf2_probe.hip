@@ -107,10 +107,11 @@ void sweep(GemmP p, int reps) {
   run<OT, 128, 8, 4, 2, 2, E>("cfg13 128x128 4w", p, reps);
   run<OT, 64, 6, 4, 2, 2, E>("cfg11 64x96 4w", p, reps);
   run<OT, 256, 10, 3, 2, 2, E>("cfg9 256x160 4w", p, reps);
-  run<OT, 64, 6, 4, 2, 2, E, 0, 0, 2>("cfg11 ks2", p, reps);
-  run<OT, 64, 6, 4, 2, 2, E, 0, 0, 3>("cfg11 ks3", p, reps);
-  run<OT, 128, 4, 3, 2, 2, E, 0, 0, 2>("cfg3 ks2", p, reps);
-  run<OT, 128, 4, 3, 2, 2, E, 0, 0, 4>("cfg3 ks4", p, reps);
+  run<OT, 64, 8, 4, 4, 2, E>("8w 64x128 ns4", p, reps);
+  run<OT, 64, 4, 4, 4, 2, E>("8w 64x64 ns4", p, reps);
+  run<OT, 64, 4, 6, 4, 2, E>("8w 64x64 ns6", p, reps);
+  run<OT, 128, 4, 4, 4, 2, E>("8w 128x64 ns4", p, reps);
+  run<OT, 64, 8, 4, 2, 4, E>("8w 64x128 2x4 ns4", p, reps);
 }
 
 int main(int argc, char** argv) {
